@@ -1,0 +1,124 @@
+/*
+ * soundchunks_amd -- MI355X-native SoundChunks encode hot path, C ABI.
+ *
+ * Two layers, both plain C (pointers + sizes, no torch types):
+ *
+ * 1. The drop-in boundary: exactly the numeric-library surface the reference
+ *    binds in encoder/extern.pas:112-123 (yakmo_single.dll + ANN.dll).  On
+ *    x86-64 Linux stdcall/cdecl collapse to the SysV ABI.
+ *      yakmo_create / yakmo_destroy / yakmo_load_train_data /
+ *      yakmo_train_on_data / yakmo_get_centroids    -> extern.pas:112-116
+ *      ann_kdtree_create / ann_kdtree_destroy / ann_kdtree_search /
+ *      ann_kdtree_pri_search / ann_kdtree_search_multi /
+ *      ann_kdtree_pri_search_multi                   -> extern.pas:118-123
+ *    Data layout is the reference's: 2-D arrays are float** row-pointer
+ *    arrays; ann_kdtree_* keep the caller's row pointers and read the
+ *    *current* point values at every search (encoder.lpr:729-745 mutates
+ *    centroids between searches of one tree).  All arithmetic runs on the GPU.
+ *
+ * 2. Frame-level batched entry points (gsc_*): the per-query ANN ABI costs
+ *    one host<->device round trip per search, so the encoder itself calls
+ *    these, which own the whole Reduce (yakmo + KNNScanReduce) and KNNFit
+ *    loops of many frames in one launch each.
+ *
+ * Errors: functions returning int return 0 on success, <0 on failure;
+ * gsc_last_error() describes the last failure of the calling thread.  There is
+ * no CPU fallback: without a usable gfx950 device every compute call fails.
+ */
+#ifndef SOUNDCHUNKS_AMD_H
+#define SOUNDCHUNKS_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- extern.pas:112-116 (yakmo_single.dll) ----------------------------- */
+typedef struct yakmo_t yakmo_t;
+/* replaces yakmo_single.dll!yakmo_create @0x180003230 (extern.pas:112) */
+yakmo_t *yakmo_create(unsigned int k, unsigned int restartCount, int maxIter, int initType, int initSeed,
+                      int doNormalize, int isVerbose);
+/* replaces yakmo_destroy @0x180003340 (extern.pas:113) */
+void yakmo_destroy(yakmo_t *ay);
+/* replaces yakmo_load_train_data @0x180003430 (extern.pas:114); copies rows */
+void yakmo_load_train_data(yakmo_t *ay, unsigned int rowCount, unsigned int colCount, float **dataset);
+/* replaces yakmo_train_on_data @0x1800034b0 (extern.pas:115); writes labels */
+void yakmo_train_on_data(yakmo_t *ay, int *pointToCluster);
+/* replaces yakmo_get_centroids @0x180003510 (extern.pas:116) */
+void yakmo_get_centroids(yakmo_t *ay, float **centroids);
+
+/* ---- extern.pas:118-123 (ANN.dll) -------------------------------------- */
+typedef struct ann_kdtree_t ann_kdtree_t;
+/* replaces ANN.dll!ann_kdtree_create @0x180003c50 (extern.pas:118); split 0 = ANN_KD_STD */
+ann_kdtree_t *ann_kdtree_create(float **pa, int n, int dd, int bs, int split);
+/* replaces ann_kdtree_destroy @0x180003cb0 (extern.pas:119) */
+void ann_kdtree_destroy(ann_kdtree_t *akd);
+/* replaces ann_kdtree_search @0x180003cd0 (extern.pas:120): k = 1, returns index */
+int ann_kdtree_search(ann_kdtree_t *akd, float *q, float eps, float *err);
+/* replaces ann_kdtree_pri_search @0x180003d30 (extern.pas:121) */
+int ann_kdtree_pri_search(ann_kdtree_t *akd, float *q, float eps, float *err);
+/* replaces ann_kdtree_search_multi @0x180003d90 (extern.pas:122) */
+void ann_kdtree_search_multi(ann_kdtree_t *akd, int *idxs, float *errs, int cnt, float *q, float eps);
+/* replaces ann_kdtree_pri_search_multi @0x180003db0 (extern.pas:123) */
+void ann_kdtree_pri_search_multi(ann_kdtree_t *akd, int *idxs, float *errs, int cnt, float *q, float eps);
+
+/* ---- frame-level batched entry points ---------------------------------- */
+/* TEncoder options (encoder.lpr:1486-1509, 1985-1998) */
+typedef struct {
+    int bit_rate;         /* -br, default -1 */
+    int precision;        /* -pr, default 3 */
+    double low_cut;       /* -lc, default 0 (band-pass filtering unsupported) */
+    double high_cut;      /* -hc, default 24000 */
+    int chunk_bit_depth;  /* -cbd, default 8 (8 or 12) */
+    int chunk_size;       /* -cs, default 4 (4, 8 or 16) */
+    int chunks_per_frame; /* -cpf, default 4096, clamped [256, 4096] */
+    int reduce_bass_band; /* !-pbb, default 1 */
+    double vfr;           /* -vfr, default 1.0 */
+    int chunk_blend;      /* -cb, default 0 (only 0 supported) */
+    double frame_length;  /* -fl, default 4000 ms */
+    int python_reduce;    /* -py (not supported by the GPU path) */
+    int verbose;          /* -v */
+} gsc_options;
+
+void gsc_default_options(gsc_options *o);
+/* encoder.lpr argv semantics (prefix match, values glued to the flag) */
+void gsc_parse_options(gsc_options *o, int argc, const char *const *argv);
+
+/* Whole-file encode: in-memory WAV (44-byte header + PCM16) -> .gsc bytes.
+ * *out is allocated by the library; release with gsc_free(). */
+int gsc_encode_wav(const uint8_t *wav, size_t wav_len, const gsc_options *o, uint8_t **out, size_t *out_len);
+
+/* Frame-range encode (multi-GPU sharding): runs the host pre-pass on the
+ * whole file, encodes frames [frame_begin, frame_end) only and returns their
+ * concatenated TFrame.SaveStream bytes; *frame_count = total frame count. */
+int gsc_encode_wav_frames(const uint8_t *wav, size_t wav_len, const gsc_options *o, int frame_begin, int frame_end,
+                          uint8_t **out, size_t *out_len, int *frame_count);
+int gsc_count_frames(const uint8_t *wav, size_t wav_len, const gsc_options *o, int *frame_count);
+
+/* Stage entry points on host buffers (row-major), used by parity tests. */
+int gsc_yakmo_seed_means(int n, int d, const float *x, int k, float *centroids);
+int gsc_scan_reduce(int n, int d, const float *x, int k, float *centroids, int *clusters, int precision, int *iters);
+int gsc_knnfit_assign(int r, int cs, const float *cand_fwd, int n, const float *q, float eps, int *best);
+
+/* Timing of the last gsc_encode_* call on the calling thread (milliseconds),
+ * split per stage, plus average device time per launch of each kernel. */
+typedef struct {
+    double host_prepare_ms, host_frames_ms, gpu_yakmo_ms, gpu_scan_ms, gpu_knnfit_ms, host_post_ms, total_ms;
+    int frames, reduce_frames;
+    long long points, scan_passes, scan_slow;
+    long long scan_point_passes; /* sum over frames of passes * N (searches) */
+    long long knnfit_pairs;      /* sum over frames of N * 4R (query x candidate) */
+    int scan_launches, knnfit_launches;
+} gsc_timing;
+void gsc_last_timing(gsc_timing *t);
+
+int gsc_device_count(void);
+const char *gsc_last_error(void);
+void gsc_free(void *p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

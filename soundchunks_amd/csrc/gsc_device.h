@@ -1,0 +1,41 @@
+// SoundChunks MI355X encode hot path -- device-side descriptors shared by the
+// HIP kernels (gsc_kernels.hip) and the host runtime (gsc_runtime.cpp).
+//
+// All arrays live in HBM, one slab per batch of frames; a descriptor per frame
+// holds offsets into those slabs (no per-frame allocations).
+#pragma once
+#include <stdint.h>
+
+namespace gsc {
+
+constexpr int kMaxK = 4096;        // CMaxChunksPerFrame (encoder.lpr:15)
+constexpr int kMaxInternal = 4095; // internal kd nodes for K <= 4096 (heap index < 4095)
+constexpr int kScanThreads = 512;  // 8 waves, 2 per SIMD
+constexpr int kScanSlots = 8;      // kd leaves (centroids) per lane, 512*8 = 4096
+constexpr int kMaxScanIters = 100; // CMaxIterations (encoder.lpr:703)
+
+// One frame of TFrame.Reduce / KNNScanReduce work (encoder.lpr:785-913, 699-765).
+struct ReduceFrame {
+    int64_t x_off;        // Dataset: N*D floats at X + x_off (row major)
+    int64_t c_off;        // Centroids: K*D floats at C + c_off (yakmo out, scan in/out)
+    int64_t n_off;        // per-point scratch (N): clusters, d0, id, cum at +n_off
+    int64_t k_off;        // per-centroid scratch (K): counts
+    int32_t N, K;
+    int32_t iters;        // out: KNNScanReduce passes
+    int32_t slow;         // out: searches resolved by the exact DFS fallback
+    double err;           // residual of the last pass (encoder.lpr:743)
+    int32_t done;         // SameValue(err, prevErr, 10^-Precision) or 100 passes
+    int32_t pad_;
+};
+
+// One frame of TFrame.KNNFit (encoder.lpr:915-978).
+struct FitFrame {
+    int64_t cand_off;     // R*CS floats: forward candidate values (neg/rev derived)
+    int64_t q_off;        // N*CS floats: queries Single(srcData)
+    int64_t out_off;      // N ints: best candidate index f = 4c + 2neg + rev
+    int32_t R, N;
+    float eps;
+    int32_t overflow;     // out: queries whose tie set exceeds ANN's 64-NN bucket
+};
+
+}  // namespace gsc

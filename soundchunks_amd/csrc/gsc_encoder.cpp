@@ -1,0 +1,518 @@
+// Host stages of the encoder (see gsc_encoder.h).  Each function cites the
+// reference encoder/encoder.lpr lines it reproduces bit-exactly.
+#include "gsc_encoder.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "fpc_math.h"
+
+namespace gsc {
+namespace {
+
+constexpr int kMaxAttenuation = 15;  // CMaxAttenuation (encoder.lpr:14)
+
+// coeff(a) = 1 + sum_{i=0..a} i*law, accumulated left to right (encoder.lpr:1654-1656)
+inline double atten_coeff(int a, double law) {
+    double c = 1.0;
+    for (int i = 0; i <= a; ++i) c += double(i) * law;
+    return c;
+}
+
+// TEncoder.makeOutputSample (encoder.lpr:1648-1663)
+inline int16_t output_sample(double smp, int obd, double coeff, bool neg) {
+    int16_t s16 = int16_t(fpc::round(smp * double(obd) * coeff));
+    if (neg) s16 = int16_t(-int(s16));
+    int v = s16;
+    v = std::max(v, -obd + 1);
+    v = std::min(v, obd - 1);
+    return int16_t(v);
+}
+
+// TEncoder.makeFloatSample (encoder.lpr:1665-1680)
+inline double float_sample(int16_t smp, double obd, double coeff, bool neg) {
+    int16_t s16 = smp;
+    if (neg) s16 = int16_t(-int(s16));
+    double r = double(s16) / (obd * coeff);
+    if (r < -1.0) r = -1.0;
+    if (r > 1.0) r = 1.0;
+    return r;
+}
+
+// hiSmp of TEncoder.ComputeAttenuation (encoder.lpr:1687-1689)
+inline int64_t hi_sample(const double* s, int cs) {
+    int64_t hi = 0;
+    for (int i = 0; i < cs; ++i) hi = std::max(hi, fpc::ceil_pos(std::fabs(s[i] * 32767.0)));
+    return hi;
+}
+
+// ComputeAttenuation loop (encoder.lpr:1691-1697) given hiSmp
+inline int attenuation_of(int64_t hi, double law) {
+    int r = 0;
+    double coeff = 1.0;
+    do {
+        ++r;
+        coeff += double(r) * law;
+    } while (!((double(hi) * coeff > 32767.0) || (r > kMaxAttenuation)));
+    return r - 1;
+}
+
+// TChunk.ComputeDstAttributes sign/reverse heuristics (encoder.lpr:374-396)
+inline void sign_reverse(const double* s, int cs, bool* neg, bool* rev) {
+    double p1 = 0.0, p2 = 0.0;
+    for (int i = 0; i < cs; ++i)
+        if (s[i] < 0) p1 -= s[i];
+    for (int i = 0; i < cs; ++i)
+        if (s[i] > 0) p2 += s[i];
+    *neg = p1 > p2;
+    p1 = 0.0;
+    p2 = 0.0;
+    for (int i = 0; i < cs / 2; ++i) p1 += std::fabs(s[i]);
+    for (int i = cs / 2; i < cs; ++i) p2 += std::fabs(s[i]);
+    *rev = p1 > p2;
+}
+
+// exact FPC trig values for every angle the features use
+struct TrigTables {
+    int cs = 0;
+    std::vector<double> dct, dft_c, dft_s, idft_c, idft_s;
+};
+
+const TrigTables& trig_for(int cs) {
+    static TrigTables cache[17];
+    static bool ready[17] = {false};
+    TrigTables& t = cache[cs];
+    if (!ready[cs]) {  // built before worker threads start (Encoder::encode_range)
+        const double PI = 3.14159265358979323846;
+        t.cs = cs;
+        t.dct.resize(size_t(cs) * cs);
+        t.dft_c.resize(size_t(cs) * cs);
+        t.dft_s.resize(size_t(cs) * cs);
+        t.idft_c.resize(size_t(cs) * cs);
+        t.idft_s.resize(size_t(cs) * cs);
+        for (int k = 0; k < cs; ++k)
+            for (int n = 0; n < cs; ++n) {
+                t.dct[k * cs + n] = fpc::cos(PI / double(cs) * (double(n) + 0.5) * double(k));
+                const double a = ((-2.0 * PI) * double(k)) * double(n) / double(cs);
+                t.dft_c[k * cs + n] = fpc::cos(a);
+                t.dft_s[k * cs + n] = fpc::sin(a);
+                const double b = ((2.0 * PI) * double(k)) * double(n) / double(cs);
+                t.idft_c[k * cs + n] = fpc::cos(b);
+                t.idft_s[k * cs + n] = fpc::sin(b);
+            }
+        ready[cs] = true;
+    }
+    return t;
+}
+
+// TChunk.ComputeDCT: canonicalise, DCT-II, cepstrum*1e-5 (encoder.lpr:258-322,349-363,1700-1716)
+void chunk_features(const TrigTables& t, const double* src, bool neg, bool rev, float* out) {
+    const int cs = t.cs;
+    double data[16], temp[16];
+    for (int i = 0; i < cs; ++i) data[i] = src[rev ? cs - 1 - i : i] * (neg ? -1.0 : 1.0);
+    const double s0 = std::sqrt(0.5), scale = std::sqrt(2.0 / double(cs));
+    for (int k = 0; k < cs; ++k) {
+        const double s = k == 0 ? s0 : 1.0;
+        double sum = 0.0;
+        const double* cr = &t.dct[size_t(k) * cs];
+        for (int n = 0; n < cs; ++n) sum += s * data[n] * cr[n];
+        out[k] = float(sum * scale);
+    }
+    for (int k = 0; k < cs; ++k) {
+        double re = 0.0, im = 0.0;
+        const double* cr = &t.dft_c[size_t(k) * cs];
+        const double* sr = &t.dft_s[size_t(k) * cs];
+        for (int i = 0; i < cs; ++i) {
+            re += data[i] * cr[i];
+            im += data[i] * sr[i];
+        }
+        temp[k] = re * re + im * im;
+    }
+    for (int i = 0; i < cs; ++i)
+        if (!fpc::is_zero(temp[i])) temp[i] = fpc::log10(temp[i]);
+    for (int k = 0; k < cs; ++k) {
+        double re = 0.0, im = 0.0;
+        const double* cr = &t.idft_c[size_t(k) * cs];
+        const double* sr = &t.idft_s[size_t(k) * cs];
+        for (int i = 0; i < cs; ++i) {
+            re += temp[i] * cr[i];
+            im += temp[i] * sr[i];
+        }
+        re /= double(cs);
+        im /= double(cs);
+        out[cs + k] = float(std::sqrt(re * re + im * im) * 0.00001);
+    }
+}
+
+// FPC TFPSList.QuickSort (encoder.exe @0x10003d410) on `items`, count descending
+void fpc_quicksort(int* items, const int* count, int L, int R) {
+    int I, J, P;
+    do {
+        I = L;
+        J = R;
+        P = (L + R) >> 1;
+        do {
+            const int pivot = count[items[P]];
+            while (count[items[I]] > pivot) ++I;
+            while (count[items[J]] < pivot) --J;
+            if (I <= J) {
+                std::swap(items[I], items[J]);
+                if (P == I) P = J;
+                else if (P == J) P = I;
+                ++I;
+                --J;
+            }
+        } while (I <= J);
+        if (L < J) fpc_quicksort(items, count, L, J);
+        L = I;
+    } while (I < R);
+}
+
+inline int bsr_word(unsigned v) {
+    int r = 0;
+    while (v >>= 1) ++r;
+    return r;
+}
+
+}  // namespace
+
+void warm_trig_tables(int cs) { (void)trig_for(cs); }
+
+// TEncoder.Load + PrepareFrames (encoder.lpr:1111-1152, 1241-1273, 1294-1429)
+int Encoder::prepare(const uint8_t* wav, size_t len, std::string* err) {
+    if (len < 44) {
+        *err = "WAV shorter than its 44-byte header";
+        return -1;
+    }
+    sample_rate_ = int(uint32_t(wav[0x18]) | (uint32_t(wav[0x19]) << 8) | (uint32_t(wav[0x1a]) << 16) |
+                       (uint32_t(wav[0x1b]) << 24));
+    channels_ = int(wav[0x16] | (wav[0x17] << 8));
+    if (channels_ <= 0 || sample_rate_ <= 0) {
+        *err = "invalid channel count or sample rate";
+        return -1;
+    }
+    const gsc_options& o = opt_;
+    if (o.chunk_blend != 0) {
+        *err = "ChunkBlend != 0 is not supported (decoder.lpr asserts it is 0)";
+        return -2;
+    }
+    if (o.python_reduce) {
+        *err = "-py (cluster.py Birch reducer) is not part of the GPU path";
+        return -2;
+    }
+    if (!(o.chunk_bit_depth == 8 || o.chunk_bit_depth == 12)) {
+        *err = "ChunkBitDepth must be 8 or 12 (TFrame.SaveStream)";
+        return -2;
+    }
+    if (!(o.chunk_size == 4 || o.chunk_size == 8 || o.chunk_size == 16)) {
+        *err = "ChunkSize must be 4, 8 or 16";
+        return -2;
+    }
+    const int cs = o.chunk_size, ch = channels_;
+    const int sc = int((len - 44) / (2 * size_t(ch)));
+    const double hc = std::min(o.high_cut, double(sample_rate_) / 2);
+    const double fcl = o.low_cut / double(sample_rate_), fch = hc / double(sample_rate_);
+    if (fcl > 0.0 || fch < 0.5) {
+        *err = "band-pass filtering (-lc/-hc below Nyquist) is not supported";
+        return -2;
+    }
+    const int under = int(std::max<int64_t>(1, fpc::round(0.25 / fch)));
+    block_ = under * (cs - o.chunk_blend);
+    sample_count_ = ((sc - 1) / block_ + 1) * block_;  // Pascal div truncates
+    const int SC = sample_count_;
+    filtered_.assign(size_t(ch), std::vector<double>(size_t(std::max(SC, 1)), 0.0));
+    const uint8_t* d = wav + 44;
+    for (int i = 0; i < sc; ++i)
+        for (int c = 0; c < ch; ++c) {
+            const uint8_t* b = d + (size_t(i) * ch + c) * 2;
+            filtered_[c][i] = double(int16_t(uint16_t(b[0] | (b[1] << 8)))) / 32767.0;
+        }
+    const int frame_count = int(fpc::ceil_pos(double(SC) / (double(sample_rate_) * (o.frame_length / 1000.0))));
+    // ChunksPerFrame search only changes anything with -br (encoder.lpr:1337-1351)
+    int cpf = o.chunks_per_frame;
+    if (o.bit_rate > 0) {
+        const long long projected =
+            (long long)std::ceil((double(SC) / double(sample_rate_)) * (double(o.bit_rate) * 1024.0 / 8.0));
+        ++cpf;
+        for (;;) {
+            --cpf;
+            const double band = (double(SC) * double(ch) * (std::log2(double(cpf)) + 3 + 1 + 1)) /
+                                (8.0 * double(cs - o.chunk_blend) * double(under));
+            const double frame = double(cpf * cs) * double(o.chunk_bit_depth) / 8.0 + double(cpf) * 4.0 / 8.0 + 16;
+            const int32_t tent = int32_t(fpc::round(0.0 + band * 0.8 + double(frame_count) * frame));
+            if (tent <= projected || cpf <= 1) break;
+        }
+        opt_.chunks_per_frame = cpf;
+    }
+    // pass 2: RMS-power balanced frame boundaries, sequential f64 (encoder.lpr:1374-1425)
+    double avg = 0.0;
+    for (int j = 0; j < ch; ++j) {
+        const double* f = filtered_[j].data();
+        for (int i = 0; i < SC; ++i) avg += f[i] * f[i];
+    }
+    avg = std::sqrt(avg / double(SC * ch));
+    std::vector<double> pw(static_cast<size_t>(std::max(SC, 1)));
+    double total = 0.0;
+    for (int i = 0; i < SC; ++i) {
+        double s = 0.0;
+        for (int j = 0; j < ch; ++j) s += filtered_[j][i] * filtered_[j][i];
+        s = std::sqrt(s / double(ch));
+        pw[i] = 1.0 - (avg + (s - avg) * o.vfr);
+        total += pw[i];
+    }
+    const double per_frame = total / double(frame_count);
+    fr_start_.clear();
+    fr_end_.clear();
+    int next = 0;
+    double cur = 0.0;
+    for (int i = 0; i < SC; ++i) {
+        cur += pw[i];
+        if ((i % block_ == 0) && (cur >= per_frame)) {
+            fr_start_.push_back(next);
+            fr_end_.push_back(i - 1);
+            cur = 0.0;
+            next = i;
+        }
+    }
+    fr_start_.push_back(next);
+    fr_end_.push_back(SC - 1);
+    return 0;
+}
+
+// FindAttenuationDivider (encoder.lpr:566-605) + MakeChunks features (467-485, 349-363)
+void Encoder::frame_host_prepare(FrameState& f) const {
+    const int cs = opt_.chunk_size, ch = channels_, bd = opt_.chunk_bit_depth;
+    const int sc = f.sample_count;
+    const int obd = (1 << (bd - 1)) - 1;
+    // --- attenuation divider: hiSmp per chunk is law-independent ---
+    const int nck = sc / cs;
+    std::vector<int64_t> hi(size_t(ch) * std::max(nck, 1));
+    for (int j = 0; j < ch; ++j)
+        for (int k = 0; k < nck; ++k) hi[size_t(j) * nck + k] = hi_sample(&filtered_[j][f.start + k * cs], cs);
+    int best_div = 1;
+    double best = 3.4028234663852886e+38;  // MaxSingle
+    std::vector<double> fs_tab(size_t(16) * (2 * obd + 1));
+    double coeff[16];
+    for (int i = 1; i <= 64; ++i) {
+        const double law = 1.0 / double(i);
+        for (int a = 0; a < 16; ++a) {
+            coeff[a] = atten_coeff(a, law);
+            for (int s = -obd; s <= obd; ++s)
+                fs_tab[size_t(a) * (2 * obd + 1) + (s + obd)] = float_sample(int16_t(s), double(obd), coeff[a], false);
+        }
+        double v = 0.0;
+        for (int j = 0; j < ch; ++j) {
+            const double* src = &filtered_[j][f.start];
+            for (int k = 0; k < nck; ++k) {
+                const int a = attenuation_of(hi[size_t(j) * nck + k], law);
+                const double* tab = &fs_tab[size_t(a) * (2 * obd + 1) + obd];
+                for (int l = 0; l < cs; ++l) {
+                    const double x = src[k * cs + l];
+                    const int16_t os = output_sample(x, obd, coeff[a], false);
+                    const double dd = x - tab[os];
+                    v += dd * dd;
+                }
+            }
+        }
+        if (v < best) {
+            best = v;
+            best_div = i;
+        }
+    }
+    f.atten_div = best_div;
+    // --- chunks: srcData, sign/reverse, features ---
+    const int chunk_count = (sc - 1) / cs + 1;
+    f.n = chunk_count * ch;
+    f.src.assign(size_t(f.n) * cs, 0.0);
+    f.feat.assign(size_t(f.n) * 2 * cs, 0.0f);
+    f.neg.assign(size_t(f.n), 0);
+    f.rev.assign(size_t(f.n), 0);
+    const TrigTables& t = trig_for(cs);
+    for (int i = 0; i < chunk_count; ++i)
+        for (int j = 0; j < ch; ++j) {
+            const int c = i * ch + j;
+            double* s = &f.src[size_t(c) * cs];
+            for (int k = 0; k < cs; ++k) {
+                const int pos = i * cs + k;
+                s[k] = pos >= sc ? 0.0 : 0.0 + filtered_[j][f.start + pos];
+            }
+            bool ng, rv;
+            sign_reverse(s, cs, &ng, &rv);
+            f.neg[c] = ng;
+            f.rev[c] = rv;
+            chunk_features(t, s, ng, rv, &f.feat[size_t(c) * 2 * cs]);
+        }
+}
+
+// TFrame.Reduce after the clustering (encoder.lpr:843-912)
+void Encoder::frame_reduce_post(FrameState& f, bool reduced) const {
+    const int cs = opt_.chunk_size, bd = opt_.chunk_bit_depth, D = 2 * cs;
+    const double law = 1.0 / double(f.atten_div);
+    const int obd = (1 << (bd - 1)) - 1;
+    auto make_reduced = [&](int i, const double* rs) {
+        double* dst = &f.rsrc[size_t(i) * cs];
+        std::memcpy(dst, rs, sizeof(double) * cs);
+        const int a = attenuation_of(hi_sample(dst, cs), law);
+        bool ng, rv;
+        sign_reverse(dst, cs, &ng, &rv);
+        f.ratten[i] = uint8_t(a);
+        f.rneg[i] = ng;
+        const double cf = atten_coeff(a, law);
+        for (int j = 0; j < cs; ++j) f.rdst[size_t(i) * cs + j] = output_sample(dst[j], obd, cf, ng);
+    };
+    if (reduced) {
+        const int K = opt_.chunks_per_frame, N = f.n;
+        std::vector<double> acc(size_t(K) * cs, 0.0);
+        std::vector<int> count(size_t(K), 0);
+        for (int j = 0; j < N; ++j) {
+            const int c = f.clusters[j];
+            const double* s = &f.src[size_t(j) * cs];
+            double* a = &acc[size_t(c) * cs];
+            const double sg = f.neg[j] ? -1.0 : 1.0;
+            for (int k = 0; k < cs; ++k) a[k] += s[f.rev[j] ? cs - 1 - k : k] * sg;
+            ++count[c];
+        }
+        std::vector<int> order(static_cast<size_t>(K));
+        for (int i = 0; i < K; ++i) order[i] = i;
+        if (K > 1) fpc_quicksort(order.data(), count.data(), 0, K - 1);
+        f.r = K;
+        f.rsrc.assign(size_t(K) * cs, 0.0);
+        f.rdst.assign(size_t(K) * cs, 0);
+        f.ratten.assign(size_t(K), 0);
+        f.rneg.assign(size_t(K), 0);
+        double tmp[16];
+        for (int i = 0; i < K; ++i) {
+            const int id = order[i];
+            const double y = double(count[id]);
+            for (int j = 0; j < cs; ++j) {
+                // div0 -> Single (encoder.lpr:863), nan0 (876)
+                const double v = fpc::is_zero(y) ? 0.0 : acc[size_t(id) * cs + j] / y;
+                const double sv = double(float(v));
+                tmp[j] = std::isnan(sv) ? 0.0 : sv;
+            }
+            make_reduced(i, tmp);
+        }
+        (void)D;
+    } else {
+        const int N = f.n;
+        f.r = N;
+        f.rsrc.assign(size_t(N) * cs, 0.0);
+        f.rdst.assign(size_t(N) * cs, 0);
+        f.ratten.assign(size_t(N), 0);
+        f.rneg.assign(size_t(N), 0);
+        for (int i = 0; i < N; ++i) make_reduced(i, &f.src[size_t(i) * cs]);
+    }
+}
+
+// KNNFit post: flags, prune unused, FPC QuickSort by use count, reindex (encoder.lpr:960-977)
+void Encoder::frame_knnfit_post(FrameState& f) const {
+    const int cs = opt_.chunk_size;
+    f.r_before_prune = f.r;
+    std::vector<int> use(size_t(f.r), 0);
+    f.red.assign(size_t(f.n), 0);
+    for (int i = 0; i < f.n; ++i) {
+        const int b = f.best[i];
+        f.neg[i] = (b & 2) != 0;
+        f.rev[i] = (b & 1) != 0;
+        f.red[i] = b >> 2;
+        ++use[b >> 2];
+    }
+    std::vector<int> alive;
+    alive.reserve(size_t(f.r));
+    for (int i = 0; i < f.r; ++i)
+        if (use[i] != 0) alive.push_back(i);
+    const int na = int(alive.size());
+    std::vector<int> cnt(static_cast<size_t>(std::max(na, 1))), order(static_cast<size_t>(std::max(na, 1)));
+    for (int i = 0; i < na; ++i) {
+        cnt[i] = use[alive[i]];
+        order[i] = i;
+    }
+    if (na > 1) fpc_quicksort(order.data(), cnt.data(), 0, na - 1);
+    std::vector<int> remap(size_t(f.r), -1);
+    std::vector<int16_t> ndst(size_t(std::max(na, 1)) * cs);
+    std::vector<uint8_t> natt(static_cast<size_t>(std::max(na, 1)));
+    for (int i = 0; i < na; ++i) {
+        const int o = alive[order[i]];
+        remap[o] = i;
+        std::memcpy(&ndst[size_t(i) * cs], &f.rdst[size_t(o) * cs], sizeof(int16_t) * cs);
+        natt[i] = f.ratten[o];
+    }
+    for (int i = 0; i < f.n; ++i) f.red[i] = remap[f.red[i]];
+    f.rdst.swap(ndst);
+    f.ratten.swap(natt);
+    f.r = na;
+}
+
+// TFrame.SaveStream (encoder.lpr:980-1107)
+void Encoder::frame_save(FrameState& f) const {
+    const int cs = opt_.chunk_size, bd = opt_.chunk_bit_depth, ch = channels_;
+    std::vector<uint8_t>& o = f.stream;
+    o.clear();
+    auto w8 = [&](unsigned v) { o.push_back(uint8_t(v)); };
+    auto w16 = [&](unsigned v) {
+        o.push_back(uint8_t(v));
+        o.push_back(uint8_t(v >> 8));
+    };
+    auto w32 = [&](uint32_t v) {
+        for (int i = 0; i < 4; ++i) o.push_back(uint8_t(v >> (8 * i)));
+    };
+    w16(unsigned((ch << 8) | 1));
+    w16(unsigned(f.r));
+    w16(unsigned((cs << 8) | bd));
+    w32(uint32_t((opt_.chunk_blend << 24) | sample_rate_));
+    w16(unsigned(f.atten_div));
+    for (int j = 0; j < f.r / 2; ++j) w8(unsigned((f.ratten[2 * j] << 4) | f.ratten[2 * j + 1]));
+    if (f.r & 1) w8(unsigned(f.ratten[f.r - 1] << 4));
+    if (bd == 8) {
+        for (size_t k = 0; k < size_t(f.r) * cs; ++k) w8(unsigned((f.rdst[k] + 128) & 0xff));
+    } else {
+        for (int j = 0; j < f.r; ++j) {
+            const int16_t* d = &f.rdst[size_t(j) * cs];
+            for (int k = 0; k < cs / 2; ++k) {
+                const int s1 = d[2 * k] + 2048, s2 = d[2 * k + 1] + 2048;
+                w8(unsigned(((s1 >> 4) & 0xf0) | ((s2 >> 8) & 0x0f)));
+                w8(unsigned(s1 & 0xff));
+                w8(unsigned(s2 & 0xff));
+            }
+            if (cs & 1) {
+                const int s1 = d[cs - 1] + 2048;
+                w8(unsigned((s1 >> 4) & 0xf0));
+                w8(unsigned(s1 & 0xff));
+            }
+        }
+    }
+    w32(uint32_t(f.n / ch));
+    int bit_cnt = 0;
+    uint32_t bits = 0;
+    int prev_vc = -1;
+    for (int j = 0; j < f.n; ++j) {
+        const int idx = f.red[j];
+        const int vc = idx == 0 ? 0 : bsr_word(unsigned(idx)) / 3;
+        uint64_t code = uint64_t(f.neg[j] ? 1 : 0) | (uint64_t(f.rev[j] ? 1 : 0) << 1);
+        int size = 2;
+        if (vc == prev_vc) {
+            size += 1;
+        } else {
+            code |= uint64_t(1) << size;
+            size += 1;
+            code |= uint64_t(vc) << size;
+            size += 2;
+        }
+        for (int k = vc; k >= 0; --k) {
+            code |= uint64_t((idx >> (k * 3)) & 7) << size;
+            size += 3;
+        }
+        bits = uint32_t(bits | (uint32_t(code) << bit_cnt));
+        bit_cnt += size;
+        if (bit_cnt >= 16) {
+            bit_cnt -= 16;
+            w16(bits & 0xffff);
+            bits >>= 16;
+        }
+        prev_vc = vc;
+    }
+    if (bit_cnt > 0) w16(bits & 0xffff);
+}
+
+}  // namespace gsc

@@ -1,0 +1,870 @@
+// SoundChunks encode hot path on MI355X (gfx950): hand-written HIP kernels.
+//
+//   yakmo_seed_kernel   yakmo_single.dll k-means++ seeding + seeding means
+//                       (encoder.lpr:824-828)   one wave / frame
+//   scan_reduce_kernel  TFrame.KNNScanReduce over ANN's stale kd-tree
+//                       (encoder.lpr:699-765; ANN.dll App. C.2)      one CU / frame
+//   knnfit_kernel       TFrame.KNNFit 64-NN + tie rule (encoder.lpr:915-965)
+//
+// Everything is bit-exact with the reference's SSE scalar arithmetic: no FMA
+// (built with -ffp-contract=off), IEEE f32 division/sqrt, sequential
+// reduction order wherever the reference is sequential.  No MFMA: the
+// distance sums must round term by term exactly like subss/mulss/addss.
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <stdint.h>
+
+#include "gsc_device.h"
+
+namespace gsc {
+
+__device__ __forceinline__ float fadd(float a, float b) { return __fadd_rn(a, b); }
+__device__ __forceinline__ float fsub(float a, float b) { return __fsub_rn(a, b); }
+__device__ __forceinline__ float fmul(float a, float b) { return __fmul_rn(a, b); }
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+template <typename T>
+__device__ __forceinline__ T ld_relaxed(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ============================================================================
+// yakmo k-means++ seeding (yakmo_single.dll @0x1800016f0) + centroid means
+// (@0x180002290).  One wave per frame.  Per pick: one pass over all points
+// (lanes = points), then the reference's sequential f32 prefix sum cum[]
+// (lane 0 walks the 64 values of each chunk through LDS).
+// ============================================================================
+template <int D>
+__global__ __launch_bounds__(64) void yakmo_seed_kernel(const ReduceFrame* __restrict__ frames, int nframes,
+                                                         const float* __restrict__ Xall, float* __restrict__ Call,
+                                                         float* __restrict__ f_scratch, int* __restrict__ i_scratch,
+                                                         uint32_t* __restrict__ bits_scratch) {
+    const int fi = blockIdx.x;
+    if (fi >= nframes) return;
+    const ReduceFrame fr = frames[fi];
+    const int N = fr.N, K = fr.K;
+    const float* X = Xall + fr.x_off;
+    float* C = Call + fr.c_off;
+    // scratch: per point d0, cum, norm (floats) and id (int) at n_off*4 ...
+    float* d0 = f_scratch + fr.n_off * 3;
+    float* cum = d0 + N;
+    float* norm = cum + N;
+    int* idv = i_scratch + fr.n_off;
+    uint32_t* chosen = bits_scratch + (fr.n_off >> 5) + fi;  // N/32+1 words per frame
+    float* sums = Call + fr.c_off;                            // accumulate into C, divide at the end
+    int* counts = i_scratch + fr.k_off + 0;                   // K ints (k_off region of i_scratch)
+
+    __shared__ float s_d0[64];
+    __shared__ float s_cum[64];
+    const int lane = threadIdx.x;
+
+    // yakmo point norm: norm += v*v (f32, in order) (@0x1800015cb)
+    for (int n = lane; n < N; n += 64) {
+        const float* x = X + (int64_t)n * D;
+        float s = 0.0f;
+#pragma unroll
+        for (int j = 0; j < D; ++j) s = fadd(s, fmul(x[j], x[j]));
+        norm[n] = s;
+    }
+    for (int w = lane; w <= (N >> 5); w += 64) chosen[w] = 0u;
+    __syncthreads();
+
+    uint64_t rx = 123456789ull, ry = 362436069ull, rz = 521288629ull, rw = 88675123ull;
+    float total = 0.0f;
+    for (int i = 0; i < K; ++i) {
+        const uint64_t t = rx ^ (rx << 11);
+        rx = ry;
+        ry = rz;
+        rz = rw;
+        rw = rw ^ (rw >> 19) ^ t ^ (t >> 8);
+        const float r = (float)((double)rw * 5.42101086242752217e-20);
+        uint32_t idx;
+        if (i == 0) {
+            idx = (uint32_t)(int64_t)floorf(fmul(r, (float)N));
+        } else {
+            const float target = fmul(r, total);
+            int64_t first = 0, count = N;
+            while (count > 0) {
+                const int64_t half = count >> 1;
+                const int64_t mid = first + half;
+                const float cm = ld_relaxed(cum + mid);
+                if (target > cm) {
+                    first = mid + 1;
+                    count -= half + 1;
+                } else {
+                    count = half;
+                }
+            }
+            idx = (uint32_t)(int64_t)(float)first;
+        }
+        // collision walk (@0x180001b20) and clamp (@0x180001c50)
+        while (idx < (uint32_t)N && ((ld_relaxed(chosen + (idx >> 5)) >> (idx & 31)) & 1u))
+            idx = (idx < (uint32_t)(N - 1)) ? idx + 1 : 0u;
+        if (idx >= (uint32_t)N) idx = (uint32_t)(N - 1);
+        if (lane == 0) chosen[idx >> 5] |= 1u << (idx & 31);
+        float c[D];
+        const float* xc = X + (int64_t)idx * D;
+#pragma unroll
+        for (int j = 0; j < D; ++j) c[j] = xc[j];
+        const float cn = ld_relaxed(norm + idx);
+
+        float run = 0.0f;  // lane 0 carries the running total
+        const bool last = (i == K - 1);
+        for (int base = 0; base < N; base += 64) {
+            const int n = base + lane;
+            float dn = 0.0f;
+            if (n < N) {
+                const float* x = X + (int64_t)n * D;
+                float d = fadd(fadd(cn, norm[n]), 0.0f);
+#pragma unroll
+                for (int j = 0; j < D; ++j) d = fsub(d, fmul(fadd(x[j], x[j]), c[j]));
+                dn = (i == 0) ? d : d0[n];
+                if (i == 0 || dn > d) {
+                    dn = d;
+                    d0[n] = d;
+                    idv[n] = i;
+                }
+            }
+            if (!last) {
+                s_d0[lane] = dn;
+                __syncthreads();
+                if (lane == 0) {
+                    const int cnt = min(64, N - base);
+                    for (int l = 0; l < cnt; ++l) {
+                        run = fadd(run, s_d0[l]);
+                        s_cum[l] = run;
+                    }
+                }
+                __syncthreads();
+                if (n < N) cum[n] = s_cum[lane];
+                __syncthreads();
+            }
+        }
+        total = __shfl(run, 0);
+        __syncthreads();
+    }
+    // centroid means of the seeding assignment: sum in point order (@0x180001ee0)
+    for (int k = lane; k < K * D; k += 64) sums[k] = 0.0f;
+    for (int k = lane; k < K; k += 64) counts[k] = 0;
+    __syncthreads();
+    if (lane < D) {
+        for (int n = 0; n < N; ++n) {
+            const int c = idv[n];
+            float* s = sums + (int64_t)c * D + lane;
+            *s = fadd(*s, X[(int64_t)n * D + lane]);
+        }
+    } else if (lane == D) {
+        for (int n = 0; n < N; ++n) counts[idv[n]] += 1;
+    }
+    __syncthreads();
+    for (int k = lane; k < K * D; k += 64) {
+        const float fc = (float)(int64_t)(uint32_t)counts[k / D];
+        sums[k] = sums[k] / fc;  // IEEE division; 0/0 = NaN like the DLL
+    }
+}
+
+// ============================================================================
+// KNNScanReduce with exact emulation of ANN's stale kd-tree search.
+//
+// Per pass: rebuild the ANN tree (ANN_KD_STD, bs = 1) over the centroids
+// exactly as annMaxSpread/annMedianSplit would, then for every point in
+// order: nearest by ANN DFS over the *stale* tree with *live* centroids,
+// online update of that centroid.  The 4096 centroids sit in VGPRs of the
+// 512 lanes (8 per lane, kd-leaf order), so every search evaluates all live
+// distances (bit-exact sequential f32 sums) and then proves, from the DFS
+// structure, which leaf ANN returns:
+//   c* = unique global minimum; for every far step u on c*'s root path,
+//   box'(u) < min over near-sibling subtrees before u  ==> c* is visited,
+//   hence ANN returns c*.  Otherwise an exact single-lane DFS over the
+//   already computed distances decides (rare: ~0.2-2% of searches).
+// ============================================================================
+struct ScanShared {
+    float cv[kMaxInternal + 1];
+    float lo[kMaxInternal + 1];
+    float hi[kMaxInternal + 1];
+    float dist[kMaxK];   // live distance per kd-leaf position (also build scratch)
+    int cntp[kMaxK];     // previous-pass counts (+1) by kd-leaf position: rate source
+    int cnta[kMaxK];     // this-pass counts by kd-leaf position
+    float wB[8][16];     // per-wave certificate thresholds by LCA depth
+    uint16_t pidx[kMaxK];
+    uint8_t cd[kMaxInternal + 1];
+    float bnd_lo[32], bnd_hi[32];
+    float wmin[8];
+    int wcnt[8];
+    int wpos[8];
+    int wok[8];
+    int slow_pos;
+    float slow_key;
+};
+
+// segment of heap node h (root 0, children 2h+1 / 2h+2, n_lo = n/2)
+__device__ __forceinline__ void node_segment(int h, int K, int& s, int& n, int& depth) {
+    s = 0;
+    n = K;
+    depth = 0;
+    int path = h + 1;
+    int lvl = 31 - __clz(path);
+    depth = lvl;
+    for (int l = lvl - 1; l >= 0; --l) {
+        const int half = n >> 1;
+        if ((path >> l) & 1) {
+            s += half;
+            n -= half;
+        } else {
+            n = half;
+        }
+    }
+}
+
+template <int D>
+__device__ void build_tree(ScanShared& sh, const float* __restrict__ C, int K) {
+    const int tid = threadIdx.x;
+    for (int p = tid; p < K; p += kScanThreads) sh.pidx[p] = (uint16_t)p;
+    // annEnclRect: sequential min/max from PA(0,d); NaNs never win a compare
+    if (tid < D) {
+        const int d = tid;
+        float lo = C[d], hi = C[d];
+        for (int i = 0; i < K; ++i) {
+            const float v = C[(int64_t)i * D + d];
+            if (v < lo) lo = v;
+            else if (v > hi) hi = v;
+        }
+        sh.bnd_lo[d] = lo;
+        sh.bnd_hi[d] = hi;
+    }
+    __syncthreads();
+    // split level by level; one thread per node runs ANN's exact sequential code
+    for (int level = 0; level < 12; ++level) {
+        const int first = (1 << level) - 1;
+        const int count = 1 << level;
+        for (int j = tid; j < count; j += kScanThreads) {
+            const int h = first + j;
+            if (h > kMaxInternal - 1) continue;
+            int s, n, depth;
+            node_segment(h, K, s, n, depth);
+            if (n < 2) continue;
+            uint16_t* pidx = sh.pidx + s;
+            // annMaxSpread: first dim with strictly largest spread
+            int cdim = 0;
+            float max_spr = 0.0f;
+            {
+                float mn[D], mx[D];
+                const float* p0 = C + (int64_t)pidx[0] * D;
+#pragma unroll
+                for (int d = 0; d < D; ++d) mn[d] = mx[d] = p0[d];
+                for (int i = 1; i < n; ++i) {
+                    const float* pp = C + (int64_t)pidx[i] * D;
+#pragma unroll
+                    for (int d = 0; d < D; ++d) {
+                        const float c = pp[d];
+                        if (c < mn[d]) mn[d] = c;
+                        else if (c > mx[d]) mx[d] = c;
+                    }
+                }
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    const float spr = fsub(mx[d], mn[d]);
+                    if (spr > max_spr) {
+                        max_spr = spr;
+                        cdim = d;
+                    }
+                }
+            }
+            float* val = sh.dist + s;  // cut-dim values of the segment
+            for (int i = 0; i < n; ++i) val[i] = C[(int64_t)pidx[i] * D + cdim];
+            const int n_lo = n >> 1;
+            // annMedianSplit (ANN.dll @0x180015680)
+            int l = 0, r = n - 1;
+#define PSWAP(a, b)                 \
+    {                               \
+        const uint16_t t_ = pidx[a]; \
+        pidx[a] = pidx[b];          \
+        pidx[b] = t_;               \
+        const float v_ = val[a];    \
+        val[a] = val[b];            \
+        val[b] = v_;                \
+    }
+            while (l < r) {
+                int i = (r + l) / 2;
+                int k;
+                if (val[i] > val[r]) PSWAP(i, r)
+                PSWAP(l, i);
+                const float c = val[l];
+                i = l;
+                k = r;
+                for (;;) {
+                    while (val[++i] < c) {}
+                    while (val[--k] > c) {}
+                    if (i < k) PSWAP(i, k) else break;
+                }
+                PSWAP(l, k);
+                if (k > n_lo) r = k - 1;
+                else if (k < n_lo) l = k + 1;
+                else break;
+            }
+            if (n_lo > 0) {
+                float c = val[0];
+                int k = 0;
+                for (int i = 1; i < n_lo; ++i)
+                    if (val[i] > c) {
+                        c = val[i];
+                        k = i;
+                    }
+                PSWAP(n_lo - 1, k);
+            }
+#undef PSWAP
+            const float cvv = (float)((double)fadd(val[n_lo - 1], val[n_lo]) / 2.0);
+            // node bounds: root rect narrowed by ancestors cutting the same dim
+            float lov = sh.bnd_lo[cdim], hiv = sh.bnd_hi[cdim];
+            {
+                int a = 0;
+                const int path = h + 1;
+                for (int bl = depth - 1; bl >= 0; --bl) {
+                    const int right = (path >> bl) & 1;
+                    if (sh.cd[a] == cdim) {
+                        if (right) lov = sh.cv[a];
+                        else hiv = sh.cv[a];
+                    }
+                    a = 2 * a + 1 + right;
+                }
+            }
+            sh.cd[h] = (uint8_t)cdim;
+            sh.cv[h] = cvv;
+            sh.lo[h] = lov;
+            sh.hi[h] = hiv;
+        }
+        __syncthreads();
+    }
+}
+
+// depth of the lowest common ancestor of kd-leaf positions p and q (p != q)
+__device__ __forceinline__ int lca_depth(int p, int q, int K, int log2K, bool pow2) {
+    if (pow2) return __clz(p ^ q) - (32 - log2K);
+    int s = 0, n = K, depth = 0;
+    for (;;) {
+        const int half = n >> 1;
+        const bool a = p >= s + half, b = q >= s + half;
+        if (a != b) return depth;
+        if (a) {
+            s += half;
+            n -= half;
+        } else {
+            n = half;
+        }
+        ++depth;
+    }
+}
+
+struct MinRec {
+    float v;
+    int cnt;
+    int pos;
+};
+__device__ __forceinline__ MinRec min_combine(MinRec a, MinRec b) {
+    if (b.v < a.v) return b;
+    if (a.v < b.v) return a;
+    MinRec r;
+    r.v = a.v;
+    r.cnt = a.cnt + b.cnt;
+    r.pos = min(a.pos, b.pos);
+    return r;
+}
+
+// Exact ANN ann_search (k = 1, eps = 0) over the stale tree with the live
+// distances already in sh.dist.  Single lane.  For a NaN leaf visited while
+// the result list is still empty, ANN's early exit depends on the partial sum
+// before the first NaN term; that is recomputed from the live mirror in C.
+template <int D>
+__device__ __noinline__ void scan_exact_dfs(ScanShared& sh, const float (&q)[D], int K, const float* __restrict__ C) {
+    int st_h[16], st_s[16], st_n[16];
+    float st_box[16];
+    int sp = 0, nmk = 0, best = -1;
+    float key = FLT_MAX;
+    float cur_box = 0.0f;
+    for (int d = 0; d < D; ++d) {
+        if (q[d] < sh.bnd_lo[d]) {
+            const float t = fsub(sh.bnd_lo[d], q[d]);
+            cur_box = fadd(cur_box, fmul(t, t));
+        } else if (q[d] > sh.bnd_hi[d]) {
+            const float t = fsub(q[d], sh.bnd_hi[d]);
+            cur_box = fadd(cur_box, fmul(t, t));
+        }
+    }
+    int h = 0, s = 0, n = K;
+    for (;;) {
+        if (n == 1) {
+            // ANNkd_leaf::ann_search: skipped iff some partial sum exceeds min_dist
+            const float dd = sh.dist[s];
+            const float min_dist = nmk == 1 ? key : FLT_MAX;
+            float chk = dd;
+            if (dd != dd) {
+                const float* c = C + (int64_t)sh.pidx[s] * D;
+                float pr = 0.0f;
+                for (int d = 0; d < D; ++d) {
+                    const float t = fsub(q[d], c[d]);
+                    const float sq = fmul(t, t);
+                    if (sq != sq) break;
+                    pr = fadd(pr, sq);
+                }
+                chk = pr;
+            }
+            if (!(chk > min_dist)) {
+                if (nmk == 0) {
+                    key = dd;
+                    best = s;
+                    nmk = 1;
+                } else if (key > dd) {
+                    key = dd;
+                    best = s;
+                }
+            }
+            // return up the recursion: far child visited iff box' < max_key
+            bool found = false;
+            while (sp > 0) {
+                --sp;
+                const float mk = nmk == 1 ? key : FLT_MAX;
+                if ((double)st_box[sp] < (double)mk) {
+                    h = st_h[sp];
+                    s = st_s[sp];
+                    n = st_n[sp];
+                    cur_box = st_box[sp];
+                    found = true;
+                    break;
+                }
+            }
+            if (!found) break;
+            continue;
+        }
+        // ANNkd_split::ann_search: descend near child, remember far child + box'
+        const int half = n >> 1;
+        const int cdim = sh.cd[h];
+        const float qc = q[cdim];
+        const float cut = fsub(qc, sh.cv[h]);
+        float bd;
+        int nh, ns, nn;
+        if (cut < 0.0f) {
+            bd = fsub(sh.lo[h], qc);
+            nh = 2 * h + 1;
+            ns = s;
+            nn = half;
+            st_h[sp] = 2 * h + 2;
+            st_s[sp] = s + half;
+            st_n[sp] = n - half;
+        } else {
+            bd = fsub(qc, sh.hi[h]);
+            nh = 2 * h + 2;
+            ns = s + half;
+            nn = n - half;
+            st_h[sp] = 2 * h + 1;
+            st_s[sp] = s;
+            st_n[sp] = half;
+        }
+        if (bd < 0.0f) bd = 0.0f;
+        st_box[sp] = fadd(cur_box, fsub(fmul(cut, cut), fmul(bd, bd)));
+        ++sp;
+        h = nh;
+        s = ns;
+        n = nn;
+    }
+    sh.slow_pos = best;
+    sh.slow_key = key;
+}
+
+// One KNNScanReduce pass (encoder.lpr:725-761) for every frame of the batch;
+// the host launches it until every frame converged (<= 100 passes).  Frames
+// that already converged return immediately.
+template <int D>
+__global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __restrict__ frames, int nframes,
+                                                                  const float* __restrict__ Xall,
+                                                                  float* __restrict__ Call, int* __restrict__ i_scratch,
+                                                                  const float* __restrict__ rate_tab, double tol,
+                                                                  int pass) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    ScanShared& sh = *reinterpret_cast<ScanShared*>(smem);
+    const int fi = blockIdx.x;
+    if (fi >= nframes) return;
+    ReduceFrame* frp = frames + fi;
+    if (frp->done) return;
+    const int N = frp->N, K = frp->K;
+    const float* X = Xall + frp->x_off;
+    float* C = Call + frp->c_off;
+    int* clusters = i_scratch + frp->n_off;
+    int* prev_cnt = i_scratch + frp->k_off;  // cnts[not Odd(iter)] by centroid id
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool pow2 = (K & (K - 1)) == 0;
+    const int log2K = 31 - __clz(K);
+
+    if (pass == 0)
+        for (int k = tid; k < K; k += kScanThreads) prev_cnt[k] = 1;  // CCntStart (encoder.lpr:717-721)
+    __syncthreads();
+    build_tree<D>(sh, C, K);
+
+    float creg[kScanSlots][D];
+    const int p0 = tid * kScanSlots;  // kd-leaf positions [p0, p0+8) live in this lane
+#pragma unroll
+    for (int s = 0; s < kScanSlots; ++s) {
+        const int p = p0 + s;
+        if (p < K) {
+            const int id = sh.pidx[p];
+#pragma unroll
+            for (int d = 0; d < D; ++d) creg[s][d] = C[(int64_t)id * D + d];
+            sh.cntp[p] = prev_cnt[id];
+            sh.cnta[p] = 1;
+        } else {
+#pragma unroll
+            for (int d = 0; d < D; ++d) creg[s][d] = 0.0f;
+        }
+    }
+    __syncthreads();
+
+    double err = 0.0;  // thread 0
+    int slow_total = 0;
+    for (int i = 0; i < N; ++i) {
+        const float* qp = X + (int64_t)i * D;
+        float q[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) q[d] = qp[d];
+        const float qlane = qp[lane & (D - 1)];
+        // ---- phase A: live distances of this lane's 8 kd leaves ----
+        float dv[kScanSlots];
+#pragma unroll
+        for (int s = 0; s < kScanSlots; ++s) dv[s] = 0.0f;
+        // ANN leaf distance: dist = dist + (q[d]-p[d])^2 for d = 0..D-1
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const float qd = q[d];
+#pragma unroll
+            for (int s = 0; s < kScanSlots; ++s) {
+                const float t = fsub(qd, creg[s][d]);
+                dv[s] = fadd(dv[s], fmul(t, t));
+            }
+        }
+        MinRec m;
+        m.v = __builtin_inff();
+        m.cnt = 0;
+        m.pos = 0x7fffffff;
+#pragma unroll
+        for (int s = 0; s < kScanSlots; ++s) {
+            const int p = p0 + s;
+            if (p < K) {
+                sh.dist[p] = dv[s];
+                if (dv[s] < m.v) {
+                    m.v = dv[s];
+                    m.cnt = 1;
+                    m.pos = p;
+                } else if (dv[s] == m.v) {
+                    m.cnt += 1;
+                }
+            }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            MinRec o;
+            o.v = __shfl_xor(m.v, off);
+            o.cnt = __shfl_xor(m.cnt, off);
+            o.pos = __shfl_xor(m.pos, off);
+            m = min_combine(m, o);
+        }
+        if (lane == 0) {
+            sh.wmin[wave] = m.v;
+            sh.wcnt[wave] = m.cnt;
+            sh.wpos[wave] = m.pos;
+        }
+        __syncthreads();
+        // ---- phase B: certificate that ANN's DFS visits the global minimum ----
+        MinRec g;
+        g.v = sh.wmin[0];
+        g.cnt = sh.wcnt[0];
+        g.pos = sh.wpos[0];
+#pragma unroll
+        for (int w = 1; w < kScanThreads / 64; ++w) {
+            MinRec o;
+            o.v = sh.wmin[w];
+            o.cnt = sh.wcnt[w];
+            o.pos = sh.wpos[w];
+            g = min_combine(g, o);
+        }
+        bool fast = (g.cnt == 1) && (g.v <= FLT_MAX);
+        const int pstar = g.pos;
+        if (fast) {
+            // annBoxDistance(q, bnd_lo, bnd_hi) of this pass's tree
+            float box = 0.0f;
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                if (q[d] < sh.bnd_lo[d]) {
+                    const float t = fsub(sh.bnd_lo[d], q[d]);
+                    box = fadd(box, fmul(t, t));
+                } else if (q[d] > sh.bnd_hi[d]) {
+                    const float t = fsub(q[d], sh.bnd_hi[d]);
+                    box = fadd(box, fmul(t, t));
+                }
+            }
+            // walk c*'s root path: box' at far steps (ANNkd_split::ann_search)
+            uint32_t farmask = 0;
+            float boxp[12];
+            int h = 0, s = 0, n = K;
+#pragma unroll
+            for (int l = 0; l < 12; ++l) {
+                boxp[l] = -__builtin_inff();
+                if (n >= 2) {
+                    const int half = n >> 1;
+                    const bool golo = pstar < s + half;
+                    const int cdim = sh.cd[h];
+                    const float qc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qlane), cdim));
+                    const float cut = fsub(qc, sh.cv[h]);
+                    const bool nearlo = cut < 0.0f;
+                    if (golo != nearlo) {
+                        float bd = nearlo ? fsub(sh.lo[h], qc) : fsub(qc, sh.hi[h]);
+                        if (bd < 0.0f) bd = 0.0f;
+                        box = fadd(box, fsub(fmul(cut, cut), fmul(bd, bd)));
+                        farmask |= 1u << l;
+                        boxp[l] = box;
+                    }
+                    if (golo) {
+                        h = 2 * h + 1;
+                        n = half;
+                    } else {
+                        h = 2 * h + 2;
+                        s += half;
+                        n -= half;
+                    }
+                }
+            }
+            // B[l] = max box' over far steps at depth >= l
+            float run = -__builtin_inff();
+#pragma unroll
+            for (int l = 11; l >= 0; --l) {
+                run = fmaxf(run, boxp[l]);
+                if (lane == 0) sh.wB[wave][l] = run;
+            }
+            // every leaf x in the near sibling of a far step u at depth l must have
+            // d(x) > B[l]; then cur(t_u) > box'(u) at every far step and ANN visits c*
+            bool ok = true;
+            const int plast = min(p0 + kScanSlots, K) - 1;
+            if (p0 < K) {
+                const bool mine = pstar >= p0 && pstar <= plast;
+                const int lv0 = mine ? -1 : lca_depth(p0, pstar, K, log2K, pow2);
+                const int lv1 = mine ? -2 : lca_depth(plast, pstar, K, log2K, pow2);
+                if (lv0 == lv1) {
+                    if ((farmask >> lv0) & 1u) {
+                        const float thr = sh.wB[wave][lv0];
+#pragma unroll
+                        for (int s2 = 0; s2 < kScanSlots; ++s2)
+                            if (p0 + s2 < K && !(dv[s2] > thr)) ok = false;
+                    }
+                } else {
+#pragma unroll
+                    for (int s2 = 0; s2 < kScanSlots; ++s2) {
+                        const int p = p0 + s2;
+                        if (p >= K || p == pstar) continue;
+                        const int lv = lca_depth(p, pstar, K, log2K, pow2);
+                        if (((farmask >> lv) & 1u) && !(dv[s2] > sh.wB[wave][lv])) ok = false;
+                    }
+                }
+            }
+            fast = __all(ok);
+        }
+        if (lane == 0) sh.wok[wave] = fast ? 1 : 0;
+        __syncthreads();
+        bool allok = true;
+#pragma unroll
+        for (int w = 0; w < kScanThreads / 64; ++w) allok = allok && (sh.wok[w] != 0);
+        int bpos;
+        float bkey;
+        if (allok) {
+            bpos = pstar;
+            bkey = g.v;
+        } else {
+            if (tid == 0) scan_exact_dfs<D>(sh, q, K, C);
+            __syncthreads();
+            bpos = sh.slow_pos;
+            bkey = sh.slow_key;
+            ++slow_total;
+        }
+        // ---- phase C: online update of the chosen centroid (encoder.lpr:735-744) ----
+        if (bpos >= 0) {
+            const int owner = __builtin_amdgcn_readfirstlane(bpos / kScanSlots);
+            const int slot = __builtin_amdgcn_readfirstlane(bpos - owner * kScanSlots);
+            const bool me = tid == owner;
+            const float rate = rate_tab[sh.cntp[bpos]];
+            const int id = sh.pidx[bpos];
+            // uniform branch on the slot, lane-select on the owner: the 8x16
+            // centroid block stays in VGPRs (no dynamic register indexing)
+#pragma unroll
+            for (int s = 0; s < kScanSlots; ++s) {
+                if (s == slot) {
+#pragma unroll
+                    for (int d = 0; d < D; ++d) {
+                        const float o = creg[s][d];
+                        const float nv = fadd(o, fmul(fsub(q[d], o), rate));
+                        creg[s][d] = me ? nv : o;
+                        if (me) C[(int64_t)id * D + d] = nv;  // live mirror for the exact DFS
+                    }
+                }
+            }
+            if (me) sh.cnta[bpos] += 1;
+            if (tid == 0) {
+                clusters[i] = id;
+                err += (double)__fsqrt_rn(bkey / (float)D);
+            }
+        }
+    }
+    // write back the live centroids and this pass's counts (cnts[Odd(iter)])
+#pragma unroll
+    for (int s = 0; s < kScanSlots; ++s) {
+        const int p = p0 + s;
+        if (p < K) {
+            const int id = sh.pidx[p];
+#pragma unroll
+            for (int d = 0; d < D; ++d) C[(int64_t)id * D + d] = creg[s][d];
+            prev_cnt[id] = sh.cnta[p];
+        }
+    }
+    if (tid == 0) {
+        const double prev_err = pass == 0 ? 3.4028234663852886e+38 : frp->err;  // err := MaxSingle
+        const double diff = err > prev_err ? err - prev_err : prev_err - err;
+        frp->iters = pass + 1;
+        frp->slow += slow_total;
+        frp->err = err;
+        frp->done = (diff <= tol || pass + 1 >= kMaxScanIters) ? 1 : 0;
+    }
+}
+
+// ============================================================================
+// KNNFit: brute-force 64-NN equivalent with the reference tie rule.
+// Candidate f = 4c + 2neg + rev (encoder.lpr:930-938); neg variants are the
+// exact negation of the forward values (IEEE division is sign-symmetric),
+// rev variants index the chunk backwards.  Pass 1: e0 = min distance.
+// Pass 2: best = smallest f with sqrtf(e_f/CS) - sqrtf(e0/CS) <= eps; if more
+// than 64 candidates qualify, ANN's bucket order would matter -> flagged.
+// ============================================================================
+template <int CS>
+__device__ __forceinline__ void knn_chunk_dists(const float (&q)[CS], const float* v, float (&e)[4]) {
+    e[0] = e[1] = e[2] = e[3] = 0.0f;
+#pragma unroll
+    for (int j = 0; j < CS; ++j) {
+        const float vf = v[j], vr = v[CS - 1 - j];
+        const float t0 = fsub(q[j], vf), t1 = fsub(q[j], vr), t2 = fsub(q[j], -vf), t3 = fsub(q[j], -vr);
+        e[0] = fadd(e[0], fmul(t0, t0));
+        e[1] = fadd(e[1], fmul(t1, t1));
+        e[2] = fadd(e[2], fmul(t2, t2));
+        e[3] = fadd(e[3], fmul(t3, t3));
+    }
+}
+
+template <int CS>
+__global__ __launch_bounds__(256) void knnfit_kernel(FitFrame* __restrict__ frames, int nframes,
+                                                      const float* __restrict__ cand_all, const float* __restrict__ q_all,
+                                                      int* __restrict__ out_all, int tiles_per_frame, int tile_r) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* tile = reinterpret_cast<float*>(smem);
+    const int fi = blockIdx.x / tiles_per_frame;
+    const int ti = blockIdx.x - fi * tiles_per_frame;
+    if (fi >= nframes) return;
+    FitFrame* fr = frames + fi;
+    const int R = fr->R, N = fr->N;
+    const float eps = fr->eps;
+    const float* cand = cand_all + fr->cand_off;
+    if (ti * 256 >= N) return;  // whole block idle (uniform)
+    const int qi = ti * 256 + threadIdx.x;
+    const bool active = qi < N;
+    float q[CS];
+#pragma unroll
+    for (int j = 0; j < CS; ++j) q[j] = active ? q_all[fr->q_off + (int64_t)qi * CS + j] : 0.0f;
+    float e0 = __builtin_inff();
+    float s0 = 0.0f;
+    int best = -1, cnt = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int c0 = 0; c0 < R; c0 += tile_r) {
+            const int nr = min(tile_r, R - c0);
+            __syncthreads();
+            for (int k = threadIdx.x; k < nr * CS; k += 256) tile[k] = cand[(int64_t)c0 * CS + k];
+            __syncthreads();
+            for (int c = 0; c < nr; ++c) {
+                float e[4];
+                knn_chunk_dists<CS>(q, tile + c * CS, e);
+                if (pass == 0) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) e0 = (e[k] < e0) ? e[k] : e0;
+                } else {
+                    // f order: 4c+0 fwd, 4c+1 rev, 4c+2 neg fwd, 4c+3 neg rev
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const float s = __fsqrt_rn(e[k] / (float)CS);
+                        const float dlt = s0 > s ? fsub(s0, s) : fsub(s, s0);
+                        if (dlt <= eps) {
+                            if (best < 0) best = 4 * (c0 + c) + k;
+                            ++cnt;
+                        }
+                    }
+                }
+            }
+        }
+        if (pass == 0) s0 = __fsqrt_rn(e0 / (float)CS);
+    }
+    if (active) {
+        out_all[fr->out_off + qi] = (cnt > 64) ? -1 : best;
+        if (cnt > 64) atomicAdd(&fr->overflow, 1);
+    }
+}
+
+}  // namespace gsc
+
+// ---------------------------------------------------------------------------
+// launch wrappers (C linkage for the runtime translation unit)
+// ---------------------------------------------------------------------------
+using namespace gsc;
+
+extern "C" hipError_t gsc_launch_yakmo(int D, const ReduceFrame* frames, int nframes, const float* X, float* C,
+                                       float* fs, int* is, uint32_t* bits, hipStream_t st) {
+    dim3 grid(nframes), block(64);
+    switch (D) {
+    case 8: hipLaunchKernelGGL(yakmo_seed_kernel<8>, grid, block, 0, st, frames, nframes, X, C, fs, is, bits); break;
+    case 16: hipLaunchKernelGGL(yakmo_seed_kernel<16>, grid, block, 0, st, frames, nframes, X, C, fs, is, bits); break;
+    case 32: hipLaunchKernelGGL(yakmo_seed_kernel<32>, grid, block, 0, st, frames, nframes, X, C, fs, is, bits); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+extern "C" hipError_t gsc_launch_scan_pass(int D, ReduceFrame* frames, int nframes, const float* X, float* C, int* is,
+                                           const float* rate_tab, double tol, int pass, hipStream_t st) {
+    dim3 grid(nframes), block(kScanThreads);
+    const size_t shm = sizeof(ScanShared);
+    switch (D) {
+    case 8:
+        (void)hipFuncSetAttribute((const void*)scan_pass_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+        hipLaunchKernelGGL(scan_pass_kernel<8>, grid, block, shm, st, frames, nframes, X, C, is, rate_tab, tol, pass);
+        break;
+    case 16:
+        (void)hipFuncSetAttribute((const void*)scan_pass_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+        hipLaunchKernelGGL(scan_pass_kernel<16>, grid, block, shm, st, frames, nframes, X, C, is, rate_tab, tol, pass);
+        break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+extern "C" hipError_t gsc_launch_knnfit(int CS, FitFrame* frames, int nframes, int max_n, int max_r,
+                                        const float* cand, const float* q, int* out, hipStream_t st) {
+    const int tiles = (max_n + 255) / 256;
+    dim3 grid(nframes * tiles), block(256);
+    int tile_r = (128 * 1024) / (CS * (int)sizeof(float));
+    if (tile_r > max_r) tile_r = max_r;
+    if (tile_r < 1) tile_r = 1;
+    size_t shm = (size_t)tile_r * CS * sizeof(float);
+    switch (CS) {
+#define KF(CSV)                                                                                                   \
+    case CSV:                                                                                                     \
+        hipFuncSetAttribute((const void*)knnfit_kernel<CSV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm); \
+        hipLaunchKernelGGL(knnfit_kernel<CSV>, grid, block, shm, st, frames, nframes, cand, q, out, tiles, tile_r);          \
+        break;
+        KF(4)
+        KF(8)
+        KF(16)
+#undef KF
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}

@@ -1,0 +1,599 @@
+// MI355X runtime for the SoundChunks hot path: device selection, HBM slabs,
+// batched launches of the Reduce (yakmo + KNNScanReduce) and KNNFit kernels
+// over many frames at once, host thread pool for the per-frame DSP, and the
+// C ABI declared in include/soundchunks.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <strings.h>
+#include <thread>
+#include <vector>
+
+#include "../../include/soundchunks.h"
+#include "fpc_math.h"
+#include "gsc_device.h"
+#include "gsc_encoder.h"
+
+extern "C" hipError_t gsc_launch_yakmo(int D, const gsc::ReduceFrame* frames, int nframes, const float* X, float* C,
+                                       float* fs, int* is, uint32_t* bits, hipStream_t st);
+extern "C" hipError_t gsc_launch_scan_pass(int D, gsc::ReduceFrame* frames, int nframes, const float* X, float* C,
+                                           int* is, const float* rate_tab, double tol, int pass, hipStream_t st);
+extern "C" hipError_t gsc_launch_knnfit(int CS, gsc::FitFrame* frames, int nframes, int max_n, int max_r,
+                                        const float* cand, const float* q, int* out, hipStream_t st);
+
+namespace gsc {
+namespace {
+
+thread_local std::string t_err;
+thread_local gsc_timing t_tim;
+
+int fail(const std::string& m) {
+    t_err = m;
+    return -1;
+}
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess) return fail(std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// The hot path requires a gfx950 device; there is no CPU fallback.
+int ensure_device() {
+    static int state = 0;  // 0 unknown, 1 ok, -1 bad
+    static std::string why;
+    if (state == 0) {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+            why = "no HIP device visible (the MI355X hot path has no CPU fallback)";
+            state = -1;
+        } else {
+            hipDeviceProp_t p;
+            int dev = 0;
+            hipGetDevice(&dev);
+            hipGetDeviceProperties(&p, dev);
+            if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0) {
+                why = std::string("device is ") + p.gcnArchName + ", kernels are built for gfx950 only";
+                state = -1;
+            } else {
+                state = 1;
+            }
+        }
+    }
+    if (state < 0) return fail(why);
+    return 0;
+}
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    hipError_t alloc(size_t count) {
+        n = count;
+        return hipMalloc(&p, sizeof(T) * std::max<size_t>(count, 1));
+    }
+};
+
+void parallel_for(int n, int threads, const std::function<void(int)>& fn) {
+    if (threads <= 1 || n <= 1) {
+        for (int i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    std::atomic<int> next{0};
+    std::vector<std::thread> pool;
+    const int t = std::min(threads, n);
+    pool.reserve(size_t(t));
+    for (int k = 0; k < t; ++k)
+        pool.emplace_back([&] {
+            for (;;) {
+                const int i = next.fetch_add(1);
+                if (i >= n) break;
+                fn(i);
+            }
+        });
+    for (auto& th : pool) th.join();
+}
+
+int host_threads() {
+    static int n = [] {
+        const char* e = std::getenv("GSC_HOST_THREADS");
+        if (e && std::atoi(e) > 0) return std::atoi(e);
+        const unsigned hc = std::thread::hardware_concurrency();
+        return int(std::min(16u, std::max(1u, hc)));
+    }();
+    return n;
+}
+
+// IntPower(10.0, -Precision) (encoder.lpr:761)
+double scan_tolerance(int precision) {
+    if (precision <= 0) return 1.0;
+    double p = 1.0, base = 10.0;
+    int i = precision;
+    while (i > 0) {
+        while ((i & 1) == 0) {
+            i >>= 1;
+            base = base * base;
+        }
+        --i;
+        p = p * base;
+    }
+    return 1.0 / p;
+}
+
+// all KNNScanReduce passes of a batch: one launch per pass, converged frames exit early
+hipError_t launch_scan_passes(int D, ReduceFrame* dfr, int nf, const float* X, float* C, int* is, const float* rate,
+                              int precision) {
+    const double tol = scan_tolerance(precision);
+    for (int pass = 0; pass < kMaxScanIters; ++pass) {
+        const hipError_t e = gsc_launch_scan_pass(D, dfr, nf, X, C, is, rate, tol, pass, nullptr);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+// rate = Single(1/sqrt(cnt)) for cnt in [0, n] (encoder.lpr:735)
+std::vector<float> rate_table(int n) {
+    std::vector<float> t(size_t(n) + 2);
+    t[0] = 0.0f;
+    for (int c = 1; c < int(t.size()); ++c) t[c] = float(1.0 / std::sqrt(double(c)));
+    return t;
+}
+
+// ---- batched device stages --------------------------------------------------
+
+// Reduce (yakmo seeding + KNNScanReduce) for a batch of frames; X/C host arrays
+// are concatenated per frame (N_f*D and K*D floats).
+int run_reduce_batch(int D, int K, int precision, const std::vector<int>& Ns, const std::vector<float>& X,
+                     std::vector<float>* C, std::vector<int>* clusters, std::vector<int>* iters, std::vector<int>* slow,
+                     double* yakmo_ms, double* scan_ms) {
+    // launches: one yakmo launch + kMaxScanIters scan launches per batch
+    const int nf = int(Ns.size());
+    if (nf == 0) return 0;
+    if (D != 8 && D != 16) return fail("KNNScanReduce kernel supports D = 8 or 16 (ChunkSize 4 or 8)");
+    std::vector<ReduceFrame> fr(static_cast<size_t>(nf));
+    int64_t xo = 0, no = 0, maxN = 0;
+    for (int i = 0; i < nf; ++i) {
+        fr[i] = ReduceFrame{};
+        fr[i].x_off = xo;
+        fr[i].c_off = int64_t(i) * K * D;
+        fr[i].n_off = no;
+        fr[i].k_off = 0;  // filled below
+        fr[i].N = Ns[i];
+        fr[i].K = K;
+        xo += int64_t(Ns[i]) * D;
+        no += Ns[i];
+        maxN = std::max<int64_t>(maxN, Ns[i]);
+    }
+    for (int i = 0; i < nf; ++i) fr[i].k_off = no + int64_t(i) * K;
+    DevBuf<float> dX, dC, dF, dRate;
+    DevBuf<int> dI;
+    DevBuf<uint32_t> dBits;
+    DevBuf<ReduceFrame> dFr;
+    HIP_TRY(dX.alloc(size_t(xo)));
+    HIP_TRY(dC.alloc(size_t(nf) * K * D));
+    HIP_TRY(dF.alloc(size_t(no) * 3));
+    HIP_TRY(dI.alloc(size_t(no) + size_t(nf) * K));
+    HIP_TRY(dBits.alloc(size_t(no / 32) + size_t(nf) * 2 + 2));
+    HIP_TRY(dFr.alloc(size_t(nf)));
+    const std::vector<float> rt = rate_table(int(maxN));
+    HIP_TRY(dRate.alloc(rt.size()));
+    HIP_TRY(hipMemcpy(dX.p, X.data(), sizeof(float) * size_t(xo), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dRate.p, rt.data(), sizeof(float) * rt.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dFr.p, fr.data(), sizeof(ReduceFrame) * size_t(nf), hipMemcpyHostToDevice));
+    hipEvent_t e0, e1, e2;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventCreate(&e2));
+    HIP_TRY(hipEventRecord(e0, nullptr));
+    HIP_TRY(gsc_launch_yakmo(D, dFr.p, nf, dX.p, dC.p, dF.p, dI.p, dBits.p, nullptr));
+    HIP_TRY(hipEventRecord(e1, nullptr));
+    HIP_TRY(launch_scan_passes(D, dFr.p, nf, dX.p, dC.p, dI.p, dRate.p, precision));
+    HIP_TRY(hipEventRecord(e2, nullptr));
+    HIP_TRY(hipEventSynchronize(e2));
+    float t1 = 0, t2 = 0;
+    hipEventElapsedTime(&t1, e0, e1);
+    hipEventElapsedTime(&t2, e1, e2);
+    if (yakmo_ms) *yakmo_ms += t1;
+    if (scan_ms) *scan_ms += t2;
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    hipEventDestroy(e2);
+    C->resize(size_t(nf) * K * D);
+    clusters->resize(size_t(no));
+    HIP_TRY(hipMemcpy(C->data(), dC.p, sizeof(float) * C->size(), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(clusters->data(), dI.p, sizeof(int) * size_t(no), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(fr.data(), dFr.p, sizeof(ReduceFrame) * size_t(nf), hipMemcpyDeviceToHost));
+    iters->resize(size_t(nf));
+    slow->resize(size_t(nf));
+    for (int i = 0; i < nf; ++i) {
+        (*iters)[i] = fr[i].iters;
+        (*slow)[i] = fr[i].slow;
+    }
+    return 0;
+}
+
+int run_knnfit_batch(int CS, const std::vector<int>& Rs, const std::vector<int>& Ns, const std::vector<float>& eps,
+                     const std::vector<float>& cand, const std::vector<float>& q, std::vector<int>* best,
+                     double* knn_ms) {
+    const int nf = int(Ns.size());
+    if (nf == 0) return 0;
+    std::vector<FitFrame> fr(static_cast<size_t>(nf));
+    int64_t co = 0, qo = 0;
+    int maxN = 0, maxR = 0;
+    for (int i = 0; i < nf; ++i) {
+        fr[i] = FitFrame{};
+        fr[i].cand_off = co;
+        fr[i].q_off = qo;
+        fr[i].out_off = qo / CS;
+        fr[i].R = Rs[i];
+        fr[i].N = Ns[i];
+        fr[i].eps = eps[i];
+        co += int64_t(Rs[i]) * CS;
+        qo += int64_t(Ns[i]) * CS;
+        maxN = std::max(maxN, Ns[i]);
+        maxR = std::max(maxR, Rs[i]);
+    }
+    DevBuf<float> dCand, dQ;
+    DevBuf<int> dOut;
+    DevBuf<FitFrame> dFr;
+    HIP_TRY(dCand.alloc(size_t(co)));
+    HIP_TRY(dQ.alloc(size_t(qo)));
+    HIP_TRY(dOut.alloc(size_t(qo / CS)));
+    HIP_TRY(dFr.alloc(size_t(nf)));
+    HIP_TRY(hipMemcpy(dCand.p, cand.data(), sizeof(float) * size_t(co), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dQ.p, q.data(), sizeof(float) * size_t(qo), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dFr.p, fr.data(), sizeof(FitFrame) * size_t(nf), hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, nullptr));
+    HIP_TRY(gsc_launch_knnfit(CS, dFr.p, nf, maxN, maxR, dCand.p, dQ.p, dOut.p, nullptr));
+    HIP_TRY(hipEventRecord(e1, nullptr));
+    HIP_TRY(hipEventSynchronize(e1));
+    float t = 0;
+    hipEventElapsedTime(&t, e0, e1);
+    if (knn_ms) *knn_ms += t;
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    best->resize(size_t(qo / CS));
+    HIP_TRY(hipMemcpy(best->data(), dOut.p, sizeof(int) * best->size(), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(fr.data(), dFr.p, sizeof(FitFrame) * size_t(nf), hipMemcpyDeviceToHost));
+    for (int i = 0; i < nf; ++i)
+        if (fr[i].overflow > 0)
+            return fail("KNNFit: " + std::to_string(fr[i].overflow) +
+                        " queries tie with more than 64 candidates (ANN bucket order emulation pending)");
+    return 0;
+}
+
+}  // namespace
+
+// ---- Encoder::encode_range: host DSP || device hot path -------------------
+int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* err, gsc_timing* tim) {
+    if (ensure_device() != 0) {
+        *err = t_err;
+        return -1;
+    }
+    const int cs = opt_.chunk_size, D = 2 * cs, K = opt_.chunks_per_frame;
+    const int nfr = e - b;
+    std::vector<FrameState> frames(static_cast<size_t>(std::max(nfr, 0)));
+    double t0 = now_ms();
+    warm_trig_tables(cs);  // FPC trig tables, built before the workers start
+    parallel_for(nfr, host_threads(), [&](int i) {
+        FrameState& f = frames[i];
+        f.index = b + i;
+        f.start = fr_start_[b + i];
+        f.sample_count = fr_end_[b + i] - fr_start_[b + i] + 1;
+        frame_host_prepare(f);
+    });
+    double t1 = now_ms();
+    // --- Reduce on the device for frames with more chunks than ChunksPerFrame
+    std::vector<int> red_idx, Ns;
+    for (int i = 0; i < nfr; ++i)
+        if (opt_.precision > 0 && frames[i].n > K) {
+            red_idx.push_back(i);
+            Ns.push_back(frames[i].n);
+        }
+    double yak_ms = 0, scan_ms = 0, knn_ms = 0;
+    long long passes = 0, slow = 0;
+    if (!red_idx.empty()) {
+        std::vector<float> X;
+        size_t tot = 0;
+        for (int i : red_idx) tot += frames[i].feat.size();
+        X.reserve(tot);
+        for (int i : red_idx) X.insert(X.end(), frames[i].feat.begin(), frames[i].feat.end());
+        std::vector<float> C;
+        std::vector<int> cl, it, sl;
+        if (run_reduce_batch(D, K, opt_.precision, Ns, X, &C, &cl, &it, &sl, &yak_ms, &scan_ms) != 0) {
+            *err = t_err;
+            return -1;
+        }
+        size_t no = 0;
+        for (size_t j = 0; j < red_idx.size(); ++j) {
+            FrameState& f = frames[red_idx[j]];
+            f.clusters.assign(cl.begin() + long(no), cl.begin() + long(no + size_t(f.n)));
+            no += size_t(f.n);
+            f.scan_iters = it[j];
+            f.scan_slow = sl[j];
+            passes += it[j];
+            slow += sl[j];
+        }
+    }
+    double t2 = now_ms();
+    std::vector<char> is_red(size_t(nfr), 0);
+    for (int i : red_idx) is_red[i] = 1;
+    parallel_for(nfr, host_threads(), [&](int i) { frame_reduce_post(frames[i], is_red[i] != 0); });
+    // --- KNNFit on the device
+    {
+        std::vector<int> Rs(static_cast<size_t>(nfr)), Nq(static_cast<size_t>(nfr));
+        std::vector<float> eps(static_cast<size_t>(nfr));
+        std::vector<float> cand, q;
+        const int bd = opt_.chunk_bit_depth;
+        const int obd = (1 << (bd - 1)) - 1;
+        for (int i = 0; i < nfr; ++i) {
+            FrameState& f = frames[i];
+            const double law = 1.0 / double(f.atten_div);
+            Rs[i] = f.r;
+            Nq[i] = f.n;
+            // epsilon (encoder.lpr:940-943), accumulated in Single
+            float acc = 1.0f;
+            for (int j = 0; j <= 15; ++j) acc = float(double(acc) + double(j) * law);
+            const float e1 = 1.0f / (float(1 << bd) * acc);
+            const float e2 = float(1.0 / 32767.0);
+            eps[i] = e1 > e2 ? e1 : e2;
+            for (int c = 0; c < f.r; ++c) {
+                double coeff = 1.0;
+                for (int a = 0; a <= f.ratten[c]; ++a) coeff += double(a) * law;
+                for (int j = 0; j < cs; ++j) {
+                    double v = double(f.rdst[size_t(c) * cs + j]) / (double(obd) * coeff);
+                    v = std::min(1.0, std::max(-1.0, v));
+                    cand.push_back(float(v));
+                }
+            }
+            for (size_t k = 0; k < f.src.size(); ++k) q.push_back(float(f.src[k]));
+        }
+        std::vector<int> best;
+        if (run_knnfit_batch(cs, Rs, Nq, eps, cand, q, &best, &knn_ms) != 0) {
+            *err = t_err;
+            return -1;
+        }
+        size_t off = 0;
+        for (int i = 0; i < nfr; ++i) {
+            frames[i].best.assign(best.begin() + long(off), best.begin() + long(off + size_t(frames[i].n)));
+            off += size_t(frames[i].n);
+        }
+    }
+    double t3 = now_ms();
+    parallel_for(nfr, host_threads(), [&](int i) {
+        frame_knnfit_post(frames[i]);
+        frame_save(frames[i]);
+    });
+    out->clear();
+    for (auto& f : frames) out->insert(out->end(), f.stream.begin(), f.stream.end());
+    double t4 = now_ms();
+    if (tim) {
+        tim->host_frames_ms = t1 - t0;
+        tim->gpu_yakmo_ms = yak_ms;
+        tim->gpu_scan_ms = scan_ms;
+        tim->gpu_knnfit_ms = knn_ms;
+        tim->host_post_ms = (t3 - t2 - knn_ms) + (t4 - t3);
+        tim->frames = nfr;
+        tim->reduce_frames = int(red_idx.size());
+        long long pts = 0;
+        for (auto& f : frames) pts += f.n;
+        tim->points = pts;
+        tim->scan_passes = passes;
+        tim->scan_slow = slow;
+        long long pp = 0;
+        for (auto& f : frames) pp += (long long)f.scan_iters * f.n;
+        tim->scan_point_passes = pp;
+        tim->scan_launches = red_idx.empty() ? 0 : kMaxScanIters;
+        tim->knnfit_launches = 1;
+        long long cand = 0;
+        for (auto& f : frames) cand += (long long)f.n * 4 * f.r_before_prune;
+        tim->knnfit_pairs = cand;
+    }
+    return 0;
+}
+
+}  // namespace gsc
+
+// ============================================================================
+// C ABI
+// ============================================================================
+using namespace gsc;
+
+extern "C" {
+
+void gsc_default_options(gsc_options* o) {
+    std::memset(o, 0, sizeof(*o));
+    o->bit_rate = -1;
+    o->precision = 3;
+    o->low_cut = 0.0;
+    o->high_cut = 24000.0;
+    o->chunk_bit_depth = 8;
+    o->chunk_size = 4;
+    o->chunks_per_frame = 4096;
+    o->reduce_bass_band = 1;
+    o->vfr = 1.0;
+    o->chunk_blend = 0;
+    o->frame_length = 4000.0;
+}
+
+static int opt_start(int argc, const char* const* argv, const char* pfx) {
+    const size_t l = std::strlen(pfx);
+    for (int i = 0; i < argc; ++i)
+        if (std::strncmp(argv[i], pfx, l) == 0) return i;
+    return -1;
+}
+static double opt_value(int argc, const char* const* argv, const char* pfx, double def) {
+    const int i = opt_start(argc, argv, pfx);
+    if (i < 0) return def;
+    const char* s = argv[i] + std::strlen(pfx);
+    if (!*s) return def;
+    char* end = nullptr;
+    const double v = std::strtod(s, &end);
+    return (end && !*end) ? v : def;  // StrToFloatDef
+}
+static bool opt_has(int argc, const char* const* argv, const char* p) {
+    for (int i = 0; i < argc; ++i)
+        if (strcasecmp(argv[i], p) == 0) return true;
+    return false;
+}
+
+void gsc_parse_options(gsc_options* o, int argc, const char* const* argv) {
+    auto clampi = [](int64_t v, int64_t lo, int64_t hi) { return int(std::min(hi, std::max(lo, v))); };
+    o->bit_rate = int(fpc::round(opt_value(argc, argv, "-br", o->bit_rate)));
+    o->precision = int(fpc::round(opt_value(argc, argv, "-pr", o->precision)));
+    o->low_cut = opt_value(argc, argv, "-lc", o->low_cut);
+    o->high_cut = opt_value(argc, argv, "-hc", o->high_cut);
+    o->vfr = std::min(1.0, std::max(0.0, opt_value(argc, argv, "-vfr", o->vfr)));
+    o->frame_length = std::max(opt_value(argc, argv, "-fl", o->frame_length), 1.0);
+    o->chunk_bit_depth = clampi(fpc::round(opt_value(argc, argv, "-cbd", o->chunk_bit_depth)), 1, 16);
+    o->chunk_size = int(fpc::round(opt_value(argc, argv, "-cs", o->chunk_size)));
+    o->chunks_per_frame = clampi(fpc::round(opt_value(argc, argv, "-cpf", o->chunks_per_frame)), 256, 4096);
+    o->verbose = opt_has(argc, argv, "-v");
+    o->reduce_bass_band = !opt_has(argc, argv, "-pbb");
+    o->chunk_blend = clampi(fpc::round(opt_value(argc, argv, "-cb", o->chunk_blend)), 0, o->chunk_size / 2);
+    o->python_reduce = opt_has(argc, argv, "-py");
+}
+
+int gsc_count_frames(const uint8_t* wav, size_t wav_len, const gsc_options* o, int* frame_count) {
+    Encoder enc(*o);
+    std::string err;
+    if (enc.prepare(wav, wav_len, &err) != 0) return fail(err);
+    *frame_count = enc.frame_count();
+    return 0;
+}
+
+int gsc_encode_wav_frames(const uint8_t* wav, size_t wav_len, const gsc_options* o, int frame_begin, int frame_end,
+                          uint8_t** out, size_t* out_len, int* frame_count) {
+    const double t0 = now_ms();
+    t_tim = gsc_timing{};
+    Encoder enc(*o);
+    std::string err;
+    if (enc.prepare(wav, wav_len, &err) != 0) return fail(err);
+    const double t1 = now_ms();
+    const int fc = enc.frame_count();
+    if (frame_count) *frame_count = fc;
+    frame_begin = std::max(0, frame_begin);
+    frame_end = std::min(fc, frame_end < 0 ? fc : frame_end);
+    std::vector<uint8_t> bytes;
+    if (frame_end > frame_begin) {
+        if (enc.encode_range(frame_begin, frame_end, &bytes, &err, &t_tim) != 0) return fail(err);
+    }
+    *out = static_cast<uint8_t*>(std::malloc(std::max<size_t>(bytes.size(), 1)));
+    if (!bytes.empty()) std::memcpy(*out, bytes.data(), bytes.size());
+    *out_len = bytes.size();
+    t_tim.host_prepare_ms = t1 - t0;
+    t_tim.total_ms = now_ms() - t0;
+    return 0;
+}
+
+int gsc_encode_wav(const uint8_t* wav, size_t wav_len, const gsc_options* o, uint8_t** out, size_t* out_len) {
+    return gsc_encode_wav_frames(wav, wav_len, o, 0, -1, out, out_len, nullptr);
+}
+
+int gsc_yakmo_seed_means(int n, int d, const float* x, int k, float* centroids) {
+    if (ensure_device() != 0) return -1;
+    if (k >= n || k <= 0) return fail("yakmo needs 0 < k < n");
+    std::vector<float> X(x, x + size_t(n) * d), C;
+    std::vector<int> cl, it, sl;
+    // run only the seeding part: precision 0 => scan loop still runs once; use a
+    // dedicated path instead
+    const int nf = 1;
+    std::vector<ReduceFrame> fr(1);
+    fr[0] = ReduceFrame{};
+    fr[0].N = n;
+    fr[0].K = k;
+    fr[0].k_off = n;
+    DevBuf<float> dX, dC, dF;
+    DevBuf<int> dI;
+    DevBuf<uint32_t> dBits;
+    DevBuf<ReduceFrame> dFr;
+    HIP_TRY(dX.alloc(X.size()));
+    HIP_TRY(dC.alloc(size_t(k) * d));
+    HIP_TRY(dF.alloc(size_t(n) * 3));
+    HIP_TRY(dI.alloc(size_t(n) + size_t(k)));
+    HIP_TRY(dBits.alloc(size_t(n / 32) + 4));
+    HIP_TRY(dFr.alloc(1));
+    HIP_TRY(hipMemcpy(dX.p, X.data(), sizeof(float) * X.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dFr.p, fr.data(), sizeof(ReduceFrame), hipMemcpyHostToDevice));
+    HIP_TRY(gsc_launch_yakmo(d, dFr.p, nf, dX.p, dC.p, dF.p, dI.p, dBits.p, nullptr));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(centroids, dC.p, sizeof(float) * size_t(k) * d, hipMemcpyDeviceToHost));
+    (void)C;
+    (void)cl;
+    (void)it;
+    (void)sl;
+    return 0;
+}
+
+int gsc_scan_reduce(int n, int d, const float* x, int k, float* centroids, int* clusters, int precision, int* iters) {
+    if (ensure_device() != 0) return -1;
+    // same kernels as the encoder, but starting from caller-provided centroids:
+    // seed via yakmo is skipped by uploading the centroids after the yakmo launch
+    if (d != 8 && d != 16) return fail("KNNScanReduce kernel supports D = 8 or 16");
+    std::vector<ReduceFrame> fr(1);
+    fr[0] = ReduceFrame{};
+    fr[0].N = n;
+    fr[0].K = k;
+    fr[0].k_off = n;
+    DevBuf<float> dX, dC, dRate;
+    DevBuf<int> dI;
+    DevBuf<ReduceFrame> dFr;
+    HIP_TRY(dX.alloc(size_t(n) * d));
+    HIP_TRY(dC.alloc(size_t(k) * d));
+    HIP_TRY(dI.alloc(size_t(n) + size_t(k)));
+    HIP_TRY(dFr.alloc(1));
+    const std::vector<float> rt = rate_table(n);
+    HIP_TRY(dRate.alloc(rt.size()));
+    HIP_TRY(hipMemcpy(dX.p, x, sizeof(float) * size_t(n) * d, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dC.p, centroids, sizeof(float) * size_t(k) * d, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dRate.p, rt.data(), sizeof(float) * rt.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dFr.p, fr.data(), sizeof(ReduceFrame), hipMemcpyHostToDevice));
+    HIP_TRY(launch_scan_passes(d, dFr.p, 1, dX.p, dC.p, dI.p, dRate.p, precision));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(centroids, dC.p, sizeof(float) * size_t(k) * d, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(clusters, dI.p, sizeof(int) * size_t(n), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(fr.data(), dFr.p, sizeof(ReduceFrame), hipMemcpyDeviceToHost));
+    if (iters) *iters = fr[0].iters;
+    return 0;
+}
+
+int gsc_knnfit_assign(int r, int cs, const float* cand_fwd, int n, const float* q, float eps, int* best) {
+    if (ensure_device() != 0) return -1;
+    std::vector<int> Rs{r}, Ns{n}, out;
+    std::vector<float> E{eps}, C(cand_fwd, cand_fwd + size_t(r) * cs), Q(q, q + size_t(n) * cs);
+    double ms = 0;
+    if (run_knnfit_batch(cs, Rs, Ns, E, C, Q, &out, &ms) != 0) return -1;
+    std::memcpy(best, out.data(), sizeof(int) * size_t(n));
+    return 0;
+}
+
+void gsc_last_timing(gsc_timing* t) { *t = t_tim; }
+
+int gsc_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* gsc_last_error(void) { return t_err.c_str(); }
+
+void gsc_free(void* p) { std::free(p); }
+
+}  // extern "C"

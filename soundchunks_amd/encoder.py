@@ -1,0 +1,111 @@
+"""Host-side mirror of the reference ``TEncoder`` (encoder/encoder.lpr:121-196)
+for the MI355X hot path.
+
+``Encoder(argv).encode(wav_bytes)`` returns ``.gsc`` bytes, bit-identical to the
+reference encoder on the same WAV and options.  Options use the reference's
+argv syntax (values glued to the flag, prefix matching; encoder.lpr:201-227,
+1985-1998), e.g. ``Encoder(["-cs8", "-cpf4096", "-cbd8"])``.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import numpy as np
+
+from . import _lib
+
+
+def parse_options(argv: Sequence[str] = ()) -> _lib.GscOptions:
+    lib = _lib.load()
+    o = _lib.GscOptions()
+    lib.gsc_default_options(ctypes.byref(o))
+    arr = (ctypes.c_char_p * max(1, len(argv)))(*[a.encode() for a in argv])
+    lib.gsc_parse_options(ctypes.byref(o), len(argv), arr)
+    return o
+
+
+def _u8(buf: bytes):
+    a = np.frombuffer(buf, dtype=np.uint8)
+    return a, a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+class Encoder:
+    """TEncoder: Load -> PrepareFrames -> MakeFrames -> SaveStream, with
+    TFrame.Reduce / TFrame.KNNFit on the GPU."""
+
+    def __init__(self, argv: Sequence[str] = ()):
+        self.argv = list(argv)
+        self.options = parse_options(self.argv)
+
+    # ChunkSize, ChunksPerFrame, ... exposed like the TEncoder fields
+    def __getattr__(self, name):
+        opts = self.__dict__.get("options")
+        if opts is not None and name in dict(_lib.GscOptions._fields_):
+            return getattr(opts, name)
+        raise AttributeError(name)
+
+    def frame_count(self, wav: bytes) -> int:
+        lib = _lib.load()
+        arr, ptr = _u8(wav)
+        n = ctypes.c_int(0)
+        _lib.check(lib.gsc_count_frames(ptr, len(arr), ctypes.byref(self.options), ctypes.byref(n)))
+        return n.value
+
+    def encode(self, wav: bytes, frame_begin: int = 0, frame_end: int = -1) -> bytes:
+        """Encode frames [frame_begin, frame_end) (default: all) to .gsc bytes."""
+        lib = _lib.load()
+        arr, ptr = _u8(wav)
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_size_t(0)
+        fc = ctypes.c_int(0)
+        rc = lib.gsc_encode_wav_frames(ptr, len(arr), ctypes.byref(self.options), frame_begin, frame_end,
+                                       ctypes.byref(out), ctypes.byref(n), ctypes.byref(fc))
+        _lib.check(rc)
+        try:
+            return ctypes.string_at(out, n.value)
+        finally:
+            lib.gsc_free(out)
+
+    @staticmethod
+    def last_timing() -> dict:
+        t = _lib.GscTiming()
+        _lib.load().gsc_last_timing(ctypes.byref(t))
+        return {k: getattr(t, k) for k, _ in t._fields_}
+
+
+def _fp(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def _ip(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+
+
+def yakmo_seed_means(x: np.ndarray, k: int) -> np.ndarray:
+    """yakmo k-means++ seeding means on the GPU (x: N x D float32)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    c = np.zeros((k, x.shape[1]), dtype=np.float32)
+    _lib.check(_lib.load().gsc_yakmo_seed_means(x.shape[0], x.shape[1], _fp(x), k, _fp(c)))
+    return c
+
+
+def scan_reduce(x: np.ndarray, c0: np.ndarray, precision: int = 3):
+    """KNNScanReduce on the GPU; returns (centroids, clusters, passes)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    c = np.ascontiguousarray(c0, dtype=np.float32).copy()
+    cl = np.zeros(x.shape[0], dtype=np.int32)
+    it = ctypes.c_int(0)
+    _lib.check(_lib.load().gsc_scan_reduce(x.shape[0], x.shape[1], _fp(x), c.shape[0], _fp(c), _ip(cl), precision,
+                                           ctypes.byref(it)))
+    return c, cl, it.value
+
+
+def knnfit_assign(cand_fwd: np.ndarray, q: np.ndarray, eps: float) -> np.ndarray:
+    """KNNFit candidate choice f = 4c + 2neg + rev per query on the GPU."""
+    cand_fwd = np.ascontiguousarray(cand_fwd, dtype=np.float32)
+    q = np.ascontiguousarray(q, dtype=np.float32)
+    out = np.zeros(q.shape[0], dtype=np.int32)
+    _lib.check(_lib.load().gsc_knnfit_assign(cand_fwd.shape[0], cand_fwd.shape[1], _fp(cand_fwd), q.shape[0],
+                                             _fp(q), ctypes.c_float(eps), _ip(out)))
+    return out

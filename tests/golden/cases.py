@@ -1,0 +1,54 @@
+"""Golden parity cases: inputs and flags.  Expected .gsc bytes are produced by
+the C oracle (oracle/) with tests/golden/make_golden.py and committed next to
+this file; GPU tests compare the HIP path against them byte for byte.
+
+Reference inputs (data files the reference's own test corpus holds):
+  my_test_test.wav   = /root/reference/my_test/test.wav   (config C1)
+  lame_test_hihat.wav = /root/reference/lame_test/hihat.wav (corpus C4 member)
+Synthetic inputs are regenerated deterministically (soundchunks_amd.synth).
+"""
+from __future__ import annotations
+
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+
+
+def _synth(seconds, rate=44100, channels=2):
+    from soundchunks_amd.synth import synth_wav
+
+    return synth_wav(seconds, rate, channels)
+
+
+def _silence_tone(seconds=2.0, rate=44100):
+    """1/2 digital silence then a tone: exact ties / duplicate points (edge case)."""
+    from soundchunks_amd.synth import wav_header
+
+    n = int(seconds * rate)
+    t = np.arange(n) / rate
+    x = np.where(t < seconds / 2, 0.0, 0.3 * np.sin(2 * np.pi * 220 * t))
+    pcm = np.round(x * 32767).astype("<i2")
+    return wav_header(1, rate, n) + pcm.tobytes()
+
+
+def _tiny():
+    """0.02 s: fewer chunks than ChunksPerFrame -> passthrough mode (encoder.lpr:891-912)."""
+    return _synth(0.02)
+
+
+CASES = {
+    # name: (input factory, argv)
+    "c1_test_cs8_cpf256": (lambda: (HERE / "my_test_test.wav").read_bytes(), ["-cs8", "-cpf256"]),
+    "hihat_cs8_cpf256": (lambda: (HERE / "lame_test_hihat.wav").read_bytes(), ["-cs8", "-cpf256"]),
+    "hihat_cs4_default": (lambda: (HERE / "lame_test_hihat.wav").read_bytes(), ["-cpf512"]),
+    "syn2s_c2_cs8_cpf4096": (lambda: _synth(2.0), ["-cs8", "-cpf4096", "-cbd8"]),
+    "syn3s_cs8_cpf1000_cbd12": (lambda: _synth(3.0), ["-cs8", "-cpf1000", "-cbd12"]),
+    "silence_tone_cs8_cpf256": (lambda: _silence_tone(), ["-cs8", "-cpf256"]),
+    "tiny_passthrough_cs8": (lambda: _tiny(), ["-cs8", "-cpf256"]),
+}
+
+
+def golden_path(name: str) -> Path:
+    return HERE / f"{name}.gsc"

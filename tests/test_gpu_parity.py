@@ -1,0 +1,69 @@
+"""HIP path vs oracle, byte for byte (run on a real MI355X: pytest -m gpu).
+
+Stage-level parity (yakmo seeding, KNNScanReduce, KNNFit) on oracle traces
+of real frames, and whole-file .gsc parity against the committed golden
+fixtures (tests/golden, produced by the C oracle).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from golden.cases import CASES, golden_path
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+def _trace(oracle, name, frame=0):
+    make, argv = CASES[name]
+    return oracle.trace_frame(make(), argv, frame)
+
+
+@pytest.mark.parametrize("name", ["c1_test_cs8_cpf256", "silence_tone_cs8_cpf256"])
+def test_yakmo_seed_means_bit_exact(oracle, name):
+    import soundchunks_amd as sc
+
+    tr = _trace(oracle, name)
+    if tr["N"] <= tr["K"]:
+        pytest.skip("passthrough frame")
+    c = sc.yakmo_seed_means(tr["dataset"], tr["K"])
+    np.testing.assert_array_equal(_bits(c), _bits(tr["yakmo"]))
+
+
+@pytest.mark.parametrize("name", ["c1_test_cs8_cpf256", "silence_tone_cs8_cpf256", "hihat_cs4_default"])
+def test_scan_reduce_bit_exact(oracle, name):
+    import soundchunks_amd as sc
+
+    tr = _trace(oracle, name)
+    if tr["N"] <= tr["K"]:
+        pytest.skip("passthrough frame")
+    c, cl, passes = sc.scan_reduce(tr["dataset"], tr["yakmo"], precision=3)
+    assert passes == tr["scan_iters"]
+    np.testing.assert_array_equal(cl, tr["clusters"])
+    np.testing.assert_array_equal(_bits(c), _bits(tr["scan"]))
+
+
+@pytest.mark.parametrize("name", ["c1_test_cs8_cpf256", "hihat_cs8_cpf256", "silence_tone_cs8_cpf256"])
+def test_knnfit_bit_exact(oracle, name):
+    import soundchunks_amd as sc
+
+    tr = _trace(oracle, name)
+    cand = tr["knn_cand"]
+    fwd = cand[0::4]  # forward, non-negated variant of every reduced chunk
+    best = sc.knnfit_assign(fwd, tr["knn_query"], tr["knn_eps"])
+    np.testing.assert_array_equal(best, tr["knn_best"])
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_gsc_matches_golden(name):
+    import soundchunks_amd as sc
+
+    make, argv = CASES[name]
+    expected = golden_path(name).read_bytes()
+    got = sc.Encoder(argv).encode(make())
+    assert len(got) == len(expected)
+    assert got == expected
