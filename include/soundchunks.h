@@ -115,6 +115,8 @@ typedef struct {
 void gsc_last_timing(gsc_timing *t);
 
 int gsc_device_count(void);
+/* bind the calling thread to a HIP device (one process per GPU) */
+int gsc_set_device(int device);
 const char *gsc_last_error(void);
 void gsc_free(void *p);
 

@@ -87,6 +87,7 @@ SIGNATURES = {
     "gsc_knnfit_assign": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _FP, ctypes.c_int, _FP, ctypes.c_float, _IP]),
     "gsc_last_timing": (None, [ctypes.POINTER(GscTiming)]),
     "gsc_device_count": (ctypes.c_int, []),
+    "gsc_set_device": (ctypes.c_int, [ctypes.c_int]),
     "gsc_last_error": (ctypes.c_char_p, []),
     "gsc_free": (None, [ctypes.c_void_p]),
 }

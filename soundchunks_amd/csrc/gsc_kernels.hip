@@ -184,7 +184,7 @@ struct ScanShared {
     float lo[kMaxInternal + 1];
     float hi[kMaxInternal + 1];
     float dist[kMaxK];   // live distance per kd-leaf position (also build scratch)
-    int cntp[kMaxK];     // previous-pass counts (+1) by kd-leaf position: rate source
+    float rate[kMaxK];   // Single(1/sqrt(previous-pass count)) by kd-leaf position
     int cnta[kMaxK];     // this-pass counts by kd-leaf position
     float wB[8][16];     // per-wave certificate thresholds by LCA depth
     uint16_t pidx[kMaxK];
@@ -220,7 +220,8 @@ __device__ __forceinline__ void node_segment(int h, int K, int& s, int& n, int& 
 template <int D>
 __device__ void build_tree(ScanShared& sh, const float* __restrict__ C, int K) {
     const int tid = threadIdx.x;
-    for (int p = tid; p < K; p += kScanThreads) sh.pidx[p] = (uint16_t)p;
+    const int nthr = blockDim.x;
+    for (int p = tid; p < K; p += nthr) sh.pidx[p] = (uint16_t)p;
     // annEnclRect: sequential min/max from PA(0,d); NaNs never win a compare
     if (tid < D) {
         const int d = tid;
@@ -238,7 +239,7 @@ __device__ void build_tree(ScanShared& sh, const float* __restrict__ C, int K) {
     for (int level = 0; level < 12; ++level) {
         const int first = (1 << level) - 1;
         const int count = 1 << level;
-        for (int j = tid; j < count; j += kScanThreads) {
+        for (int j = tid; j < count; j += nthr) {
             const int h = first + j;
             if (h > kMaxInternal - 1) continue;
             int s, n, depth;
@@ -471,13 +472,44 @@ __device__ __noinline__ void scan_exact_dfs(ScanShared& sh, const float (&q)[D],
     sh.slow_key = key;
 }
 
+template <typename T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (T*)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int uniform_int(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// wave-wide min of non-negative f32 bit patterns (order-preserving as u32;
+// NaN sorts above +inf so it only wins when every value is NaN)
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+    const int id = -1;
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)x, 0x111, 0xf, 0xf, false));  // row_shr:1
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)x, 0x112, 0xf, 0xf, false));  // row_shr:2
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)x, 0x114, 0xf, 0xf, false));  // row_shr:4
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)x, 0x118, 0xf, 0xf, false));  // row_shr:8
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)x, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+// workgroup barrier that orders LDS only: global stores issued in the search
+// loop (cluster ids, live centroid mirror) stay in flight across it
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // One KNNScanReduce pass (encoder.lpr:725-761) for every frame of the batch;
 // the host launches it until every frame converged (<= 100 passes).  Frames
-// that already converged return immediately.
+// that already converged return immediately.  blockDim = 64 * ceil(K / 512).
 template <int D>
 __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __restrict__ frames, int nframes,
                                                                   const float* __restrict__ Xall,
                                                                   float* __restrict__ Call, int* __restrict__ i_scratch,
+                                                                  float* __restrict__ f_scratch,
                                                                   const float* __restrict__ rate_tab, double tol,
                                                                   int pass) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -485,20 +517,39 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
     const int fi = blockIdx.x;
     if (fi >= nframes) return;
     ReduceFrame* frp = frames + fi;
-    if (frp->done) return;
-    const int N = frp->N, K = frp->K;
-    const float* X = Xall + frp->x_off;
-    float* C = Call + frp->c_off;
-    int* clusters = i_scratch + frp->n_off;
-    int* prev_cnt = i_scratch + frp->k_off;  // cnts[not Odd(iter)] by centroid id
+    if (uniform_int(frp->done)) return;
+    const int N = uniform_int(frp->N), K = uniform_int(frp->K);
+    const float* __restrict__ X = uniform_ptr(Xall + frp->x_off);
+    float* C = uniform_ptr(Call + frp->c_off);
+    int* clusters = uniform_ptr(i_scratch + frp->n_off);
+    int* prev_cnt = uniform_ptr(i_scratch + frp->k_off);  // cnts[not Odd(iter)] by centroid id
+    float* box0 = uniform_ptr(f_scratch + frp->n_off * 3);  // root box per query (yakmo scratch reused)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nthreads = blockDim.x, nwaves = nthreads >> 6;
     const bool pow2 = (K & (K - 1)) == 0;
     const int log2K = 31 - __clz(K);
 
     if (pass == 0)
-        for (int k = tid; k < K; k += kScanThreads) prev_cnt[k] = 1;  // CCntStart (encoder.lpr:717-721)
+        for (int k = tid; k < K; k += nthreads) prev_cnt[k] = 1;  // CCntStart (encoder.lpr:717-721)
     __syncthreads();
     build_tree<D>(sh, C, K);
+    // annBoxDistance(q, bnd_lo, bnd_hi) for every query of this pass
+    for (int i = tid; i < N; i += nthreads) {
+        const float* qp = X + (int64_t)i * D;
+        float box = 0.0f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const float qd = qp[d];
+            if (qd < sh.bnd_lo[d]) {
+                const float t = fsub(sh.bnd_lo[d], qd);
+                box = fadd(box, fmul(t, t));
+            } else if (qd > sh.bnd_hi[d]) {
+                const float t = fsub(qd, sh.bnd_hi[d]);
+                box = fadd(box, fmul(t, t));
+            }
+        }
+        box0[i] = box;
+    }
 
     float creg[kScanSlots][D];
     const int p0 = tid * kScanSlots;  // kd-leaf positions [p0, p0+8) live in this lane
@@ -509,13 +560,16 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
             const int id = sh.pidx[p];
 #pragma unroll
             for (int d = 0; d < D; ++d) creg[s][d] = C[(int64_t)id * D + d];
-            sh.cntp[p] = prev_cnt[id];
+            sh.rate[p] = rate_tab[prev_cnt[id]];  // Single(1/sqrt(cnts[not Odd(iter)]))
             sh.cnta[p] = 1;
         } else {
 #pragma unroll
             for (int d = 0; d < D; ++d) creg[s][d] = 0.0f;
         }
     }
+    // depth of the kd tree: leaves at depth <= maxdepth
+    int maxdepth = 0;
+    while ((1 << maxdepth) < K) ++maxdepth;
     __syncthreads();
 
     double err = 0.0;  // thread 0
@@ -526,6 +580,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
 #pragma unroll
         for (int d = 0; d < D; ++d) q[d] = qp[d];
         const float qlane = qp[lane & (D - 1)];
+        const float rootbox = box0[i];
         // ---- phase A: live distances of this lane's 8 kd leaves ----
         float dv[kScanSlots];
 #pragma unroll
@@ -540,45 +595,41 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
                 dv[s] = fadd(dv[s], fmul(t, t));
             }
         }
-        MinRec m;
-        m.v = __builtin_inff();
-        m.cnt = 0;
-        m.pos = 0x7fffffff;
+        uint32_t lmin = 0xffffffffu;
+#pragma unroll
+        for (int s = 0; s < kScanSlots; ++s)
+            if (p0 + s < K) lmin = min(lmin, __float_as_uint(dv[s]));
+        const uint32_t wmin = wave_min_u32(lmin);
+        uint64_t any = 0;
+        int wcnt = 0;
+        uint64_t masks[kScanSlots];
 #pragma unroll
         for (int s = 0; s < kScanSlots; ++s) {
-            const int p = p0 + s;
-            if (p < K) {
-                sh.dist[p] = dv[s];
-                if (dv[s] < m.v) {
-                    m.v = dv[s];
-                    m.cnt = 1;
-                    m.pos = p;
-                } else if (dv[s] == m.v) {
-                    m.cnt += 1;
-                }
-            }
+            masks[s] = __ballot((p0 + s < K) && __float_as_uint(dv[s]) == wmin);
+            wcnt += __popcll(masks[s]);
+            any |= masks[s];
         }
+        int wpos = 0x7fffffff;
+        if (any) {
+            const int l = __ffsll((long long)any) - 1;
+            int slot = kScanSlots;
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            MinRec o;
-            o.v = __shfl_xor(m.v, off);
-            o.cnt = __shfl_xor(m.cnt, off);
-            o.pos = __shfl_xor(m.pos, off);
-            m = min_combine(m, o);
+            for (int s = kScanSlots - 1; s >= 0; --s)
+                if ((masks[s] >> l) & 1ull) slot = s;
+            wpos = (wave * 64 + l) * kScanSlots + slot;
         }
         if (lane == 0) {
-            sh.wmin[wave] = m.v;
-            sh.wcnt[wave] = m.cnt;
-            sh.wpos[wave] = m.pos;
+            sh.wmin[wave] = __uint_as_float(wmin);
+            sh.wcnt[wave] = wcnt;
+            sh.wpos[wave] = wpos;
         }
-        __syncthreads();
+        lds_barrier();
         // ---- phase B: certificate that ANN's DFS visits the global minimum ----
         MinRec g;
         g.v = sh.wmin[0];
         g.cnt = sh.wcnt[0];
         g.pos = sh.wpos[0];
-#pragma unroll
-        for (int w = 1; w < kScanThreads / 64; ++w) {
+        for (int w = 1; w < nwaves; ++w) {
             MinRec o;
             o.v = sh.wmin[w];
             o.cnt = sh.wcnt[w];
@@ -588,70 +639,84 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
         bool fast = (g.cnt == 1) && (g.v <= FLT_MAX);
         const int pstar = g.pos;
         if (fast) {
-            // annBoxDistance(q, bnd_lo, bnd_hi) of this pass's tree
-            float box = 0.0f;
-#pragma unroll
-            for (int d = 0; d < D; ++d) {
-                if (q[d] < sh.bnd_lo[d]) {
-                    const float t = fsub(sh.bnd_lo[d], q[d]);
-                    box = fadd(box, fmul(t, t));
-                } else if (q[d] > sh.bnd_hi[d]) {
-                    const float t = fsub(q[d], sh.bnd_hi[d]);
-                    box = fadd(box, fmul(t, t));
+            // lane l < maxdepth evaluates the split node at depth l on c*'s path
+            bool far = false;
+            float inc = 0.0f;
+            if (lane < maxdepth) {
+                int h, s, n;
+                bool golo;
+                if (pow2) {
+                    const int sh_ = log2K - lane;
+                    h = (1 << lane) - 1 + (pstar >> sh_);
+                    s = (pstar >> sh_) << sh_;
+                    n = K >> lane;
+                    golo = ((pstar >> (sh_ - 1)) & 1) == 0;
+                } else {
+                    h = 0;
+                    s = 0;
+                    n = K;
+                    for (int l = 0; l < lane && n >= 2; ++l) {
+                        const int half = n >> 1;
+                        if (pstar < s + half) {
+                            h = 2 * h + 1;
+                            n = half;
+                        } else {
+                            h = 2 * h + 2;
+                            s += half;
+                            n -= half;
+                        }
+                    }
+                    golo = pstar < s + (n >> 1);
                 }
-            }
-            // walk c*'s root path: box' at far steps (ANNkd_split::ann_search)
-            uint32_t farmask = 0;
-            float boxp[12];
-            int h = 0, s = 0, n = K;
-#pragma unroll
-            for (int l = 0; l < 12; ++l) {
-                boxp[l] = -__builtin_inff();
                 if (n >= 2) {
-                    const int half = n >> 1;
-                    const bool golo = pstar < s + half;
                     const int cdim = sh.cd[h];
-                    const float qc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qlane), cdim));
+                    const float qc = __shfl(qlane, cdim);
                     const float cut = fsub(qc, sh.cv[h]);
                     const bool nearlo = cut < 0.0f;
                     if (golo != nearlo) {
                         float bd = nearlo ? fsub(sh.lo[h], qc) : fsub(qc, sh.hi[h]);
                         if (bd < 0.0f) bd = 0.0f;
-                        box = fadd(box, fsub(fmul(cut, cut), fmul(bd, bd)));
-                        farmask |= 1u << l;
-                        boxp[l] = box;
-                    }
-                    if (golo) {
-                        h = 2 * h + 1;
-                        n = half;
-                    } else {
-                        h = 2 * h + 2;
-                        s += half;
-                        n -= half;
+                        far = true;
+                        inc = fsub(fmul(cut, cut), fmul(bd, bd));
                     }
                 }
+            } else {
+                (void)__shfl(qlane, 0);
             }
-            // B[l] = max box' over far steps at depth >= l
-            float run = -__builtin_inff();
-#pragma unroll
-            for (int l = 11; l >= 0; --l) {
-                run = fmaxf(run, boxp[l]);
-                if (lane == 0) sh.wB[wave][l] = run;
+            const uint64_t farmask = __ballot(far);
+            // box' = ((root + inc_a) + inc_b) + ... over far steps, in depth order
+            float box = rootbox;
+            float boxp = -__builtin_inff();
+            for (int l = 0; l < maxdepth; ++l) {
+                if ((farmask >> l) & 1ull) {
+                    box = fadd(box, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(inc), l)));
+                    if (lane == l) boxp = box;
+                }
             }
-            // every leaf x in the near sibling of a far step u at depth l must have
-            // d(x) > B[l]; then cur(t_u) > box'(u) at every far step and ANN visits c*
+            // B[l] = max box' over far steps at depth >= l (lane l holds B[l])
+            float B = -__builtin_inff(), run = -__builtin_inff();
+            for (int l = maxdepth - 1; l >= 0; --l) {
+                run = fmaxf(run, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(boxp), l)));
+                if (lane == l) B = run;
+            }
+            if (lane < 16) sh.wB[wave][lane] = B;  // per-wave table, read back by LCA depth
+            // every leaf x in the near sibling of a far step u at depth l needs
+            // d(x) > B[l]; then cur(t_u) > box'(u) at every far step: ANN visits c*
             bool ok = true;
             const int plast = min(p0 + kScanSlots, K) - 1;
+            const bool mine = pstar >= p0 && pstar <= plast;
+            int lv0 = 0, lv1 = 0;
+            if (p0 < K && !mine) {
+                lv0 = lca_depth(p0, pstar, K, log2K, pow2);
+                lv1 = lca_depth(plast, pstar, K, log2K, pow2);
+            }
             if (p0 < K) {
-                const bool mine = pstar >= p0 && pstar <= plast;
-                const int lv0 = mine ? -1 : lca_depth(p0, pstar, K, log2K, pow2);
-                const int lv1 = mine ? -2 : lca_depth(plast, pstar, K, log2K, pow2);
-                if (lv0 == lv1) {
-                    if ((farmask >> lv0) & 1u) {
-                        const float thr = sh.wB[wave][lv0];
+                const float thr0 = sh.wB[wave][lv0 & 15];
+                if (!mine && lv0 == lv1) {
+                    if ((farmask >> lv0) & 1ull) {
 #pragma unroll
                         for (int s2 = 0; s2 < kScanSlots; ++s2)
-                            if (p0 + s2 < K && !(dv[s2] > thr)) ok = false;
+                            if (p0 + s2 < K && !(dv[s2] > thr0)) ok = false;
                     }
                 } else {
 #pragma unroll
@@ -659,23 +724,27 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
                         const int p = p0 + s2;
                         if (p >= K || p == pstar) continue;
                         const int lv = lca_depth(p, pstar, K, log2K, pow2);
-                        if (((farmask >> lv) & 1u) && !(dv[s2] > sh.wB[wave][lv])) ok = false;
+                        if (((farmask >> lv) & 1ull) && !(dv[s2] > sh.wB[wave][lv])) ok = false;
                     }
                 }
             }
             fast = __all(ok);
         }
         if (lane == 0) sh.wok[wave] = fast ? 1 : 0;
-        __syncthreads();
+        lds_barrier();
         bool allok = true;
-#pragma unroll
-        for (int w = 0; w < kScanThreads / 64; ++w) allok = allok && (sh.wok[w] != 0);
+        for (int w = 0; w < nwaves; ++w) allok = allok && (sh.wok[w] != 0);
         int bpos;
         float bkey;
         if (allok) {
             bpos = pstar;
             bkey = g.v;
         } else {
+            // exact DFS over all live distances (rare)
+#pragma unroll
+            for (int s = 0; s < kScanSlots; ++s)
+                if (p0 + s < K) sh.dist[p0 + s] = dv[s];
+            __syncthreads();
             if (tid == 0) scan_exact_dfs<D>(sh, q, K, C);
             __syncthreads();
             bpos = sh.slow_pos;
@@ -687,9 +756,9 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
             const int owner = __builtin_amdgcn_readfirstlane(bpos / kScanSlots);
             const int slot = __builtin_amdgcn_readfirstlane(bpos - owner * kScanSlots);
             const bool me = tid == owner;
-            const float rate = rate_tab[sh.cntp[bpos]];
+            const float rate = sh.rate[bpos];
             const int id = sh.pidx[bpos];
-            // uniform branch on the slot, lane-select on the owner: the 8x16
+            // uniform branch on the slot, lane-select on the owner: the 8xD
             // centroid block stays in VGPRs (no dynamic register indexing)
 #pragma unroll
             for (int s = 0; s < kScanSlots; ++s) {
@@ -710,6 +779,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
             }
         }
     }
+    __syncthreads();
     // write back the live centroids and this pass's counts (cnts[Odd(iter)])
 #pragma unroll
     for (int s = 0; s < kScanSlots; ++s) {
@@ -828,18 +898,20 @@ extern "C" hipError_t gsc_launch_yakmo(int D, const ReduceFrame* frames, int nfr
     return hipGetLastError();
 }
 
-extern "C" hipError_t gsc_launch_scan_pass(int D, ReduceFrame* frames, int nframes, const float* X, float* C, int* is,
-                                           const float* rate_tab, double tol, int pass, hipStream_t st) {
-    dim3 grid(nframes), block(kScanThreads);
+extern "C" hipError_t gsc_launch_scan_pass(int D, ReduceFrame* frames, int nframes, int K, const float* X, float* C,
+                                           int* is, float* fs, const float* rate_tab, double tol, int pass,
+                                           hipStream_t st) {
+    const int waves = (K + 64 * kScanSlots - 1) / (64 * kScanSlots);
+    dim3 grid(nframes), block(64 * waves);
     const size_t shm = sizeof(ScanShared);
     switch (D) {
     case 8:
         (void)hipFuncSetAttribute((const void*)scan_pass_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-        hipLaunchKernelGGL(scan_pass_kernel<8>, grid, block, shm, st, frames, nframes, X, C, is, rate_tab, tol, pass);
+        hipLaunchKernelGGL(scan_pass_kernel<8>, grid, block, shm, st, frames, nframes, X, C, is, fs, rate_tab, tol, pass);
         break;
     case 16:
         (void)hipFuncSetAttribute((const void*)scan_pass_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-        hipLaunchKernelGGL(scan_pass_kernel<16>, grid, block, shm, st, frames, nframes, X, C, is, rate_tab, tol, pass);
+        hipLaunchKernelGGL(scan_pass_kernel<16>, grid, block, shm, st, frames, nframes, X, C, is, fs, rate_tab, tol, pass);
         break;
     default: return hipErrorInvalidValue;
     }

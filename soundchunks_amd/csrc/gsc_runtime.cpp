@@ -23,8 +23,9 @@
 
 extern "C" hipError_t gsc_launch_yakmo(int D, const gsc::ReduceFrame* frames, int nframes, const float* X, float* C,
                                        float* fs, int* is, uint32_t* bits, hipStream_t st);
-extern "C" hipError_t gsc_launch_scan_pass(int D, gsc::ReduceFrame* frames, int nframes, const float* X, float* C,
-                                           int* is, const float* rate_tab, double tol, int pass, hipStream_t st);
+extern "C" hipError_t gsc_launch_scan_pass(int D, gsc::ReduceFrame* frames, int nframes, int K, const float* X,
+                                           float* C, int* is, float* fs, const float* rate_tab, double tol, int pass,
+                                           hipStream_t st);
 extern "C" hipError_t gsc_launch_knnfit(int CS, gsc::FitFrame* frames, int nframes, int max_n, int max_r,
                                         const float* cand, const float* q, int* out, hipStream_t st);
 
@@ -135,11 +136,11 @@ double scan_tolerance(int precision) {
 }
 
 // all KNNScanReduce passes of a batch: one launch per pass, converged frames exit early
-hipError_t launch_scan_passes(int D, ReduceFrame* dfr, int nf, const float* X, float* C, int* is, const float* rate,
-                              int precision) {
+hipError_t launch_scan_passes(int D, ReduceFrame* dfr, int nf, int K, const float* X, float* C, int* is, float* fs,
+                              const float* rate, int precision) {
     const double tol = scan_tolerance(precision);
     for (int pass = 0; pass < kMaxScanIters; ++pass) {
-        const hipError_t e = gsc_launch_scan_pass(D, dfr, nf, X, C, is, rate, tol, pass, nullptr);
+        const hipError_t e = gsc_launch_scan_pass(D, dfr, nf, K, X, C, is, fs, rate, tol, pass, nullptr);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -201,7 +202,7 @@ int run_reduce_batch(int D, int K, int precision, const std::vector<int>& Ns, co
     HIP_TRY(hipEventRecord(e0, nullptr));
     HIP_TRY(gsc_launch_yakmo(D, dFr.p, nf, dX.p, dC.p, dF.p, dI.p, dBits.p, nullptr));
     HIP_TRY(hipEventRecord(e1, nullptr));
-    HIP_TRY(launch_scan_passes(D, dFr.p, nf, dX.p, dC.p, dI.p, dRate.p, precision));
+    HIP_TRY(launch_scan_passes(D, dFr.p, nf, K, dX.p, dC.p, dI.p, dF.p, dRate.p, precision));
     HIP_TRY(hipEventRecord(e2, nullptr));
     HIP_TRY(hipEventSynchronize(e2));
     float t1 = 0, t2 = 0;
@@ -552,9 +553,10 @@ int gsc_scan_reduce(int n, int d, const float* x, int k, float* centroids, int* 
     fr[0].N = n;
     fr[0].K = k;
     fr[0].k_off = n;
-    DevBuf<float> dX, dC, dRate;
+    DevBuf<float> dX, dC, dRate, dF;
     DevBuf<int> dI;
     DevBuf<ReduceFrame> dFr;
+    HIP_TRY(dF.alloc(size_t(n) * 3));
     HIP_TRY(dX.alloc(size_t(n) * d));
     HIP_TRY(dC.alloc(size_t(k) * d));
     HIP_TRY(dI.alloc(size_t(n) + size_t(k)));
@@ -565,7 +567,7 @@ int gsc_scan_reduce(int n, int d, const float* x, int k, float* centroids, int* 
     HIP_TRY(hipMemcpy(dC.p, centroids, sizeof(float) * size_t(k) * d, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(dRate.p, rt.data(), sizeof(float) * rt.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(dFr.p, fr.data(), sizeof(ReduceFrame), hipMemcpyHostToDevice));
-    HIP_TRY(launch_scan_passes(d, dFr.p, 1, dX.p, dC.p, dI.p, dRate.p, precision));
+    HIP_TRY(launch_scan_passes(d, dFr.p, 1, k, dX.p, dC.p, dI.p, dF.p, dRate.p, precision));
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(centroids, dC.p, sizeof(float) * size_t(k) * d, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(clusters, dI.p, sizeof(int) * size_t(n), hipMemcpyDeviceToHost));
@@ -585,6 +587,11 @@ int gsc_knnfit_assign(int r, int cs, const float* cand_fwd, int n, const float* 
 }
 
 void gsc_last_timing(gsc_timing* t) { *t = t_tim; }
+
+int gsc_set_device(int device) {
+    HIP_TRY(hipSetDevice(device));
+    return 0;
+}
 
 int gsc_device_count(void) {
     int n = 0;

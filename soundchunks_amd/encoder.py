@@ -74,6 +74,11 @@ class Encoder:
         return {k: getattr(t, k) for k, _ in t._fields_}
 
 
+def set_device(device: int) -> None:
+    """Bind this process's HIP context to `device` (one process per GPU)."""
+    _lib.check(_lib.load().gsc_set_device(device))
+
+
 def _fp(a: np.ndarray):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
 
