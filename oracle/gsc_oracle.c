@@ -814,7 +814,7 @@ static void do_frame(const enc_t *e, int fi, buf_t *o, frame_t *keep, reduce_tra
 typedef struct {
     const enc_t *e;
     buf_t *outs;
-    int next;
+    int next, end;
     pthread_mutex_t mu;
 } pool_t;
 
@@ -824,13 +824,18 @@ static void *worker(void *arg) {
         pthread_mutex_lock(&pl->mu);
         int fi = pl->next++;
         pthread_mutex_unlock(&pl->mu);
-        if (fi >= pl->e->frame_count) break;
+        if (fi >= pl->end) break;
         do_frame(pl->e, fi, &pl->outs[fi], NULL, NULL, NULL);
     }
     return NULL;
 }
 
-int ora_encode(const uint8_t *wav, size_t wav_len, const gsc_params *p, int threads, uint8_t **out, size_t *out_len) {
+/* Frames [frame_begin, frame_end) of the whole-file encode (frame_end < 0 =>
+ * all); their TFrame.SaveStream bytes concatenated in frame order
+ * (encoder.lpr:1181-1215 writes frames in order).  Used by the multi-rank
+ * sharding tests: the concatenation over ranks equals ora_encode. */
+int ora_encode_frames(const uint8_t *wav, size_t wav_len, const gsc_params *p, int frame_begin, int frame_end,
+                      int threads, uint8_t **out, size_t *out_len, int *frame_count) {
     enc_t e;
     memset(&e, 0, sizeof(e));
     e.p = *p;
@@ -839,18 +844,23 @@ int ora_encode(const uint8_t *wav, size_t wav_len, const gsc_params *p, int thre
         enc_free(&e);
         return rc;
     }
+    if (frame_count) *frame_count = e.frame_count;
+    if (frame_begin < 0) frame_begin = 0;
+    if (frame_end < 0 || frame_end > e.frame_count) frame_end = e.frame_count;
     (void)get_trig(e.p.chunk_size);
     pthread_mutex_lock(&g_stats_mu);
     memset(&g_stats, 0, sizeof(g_stats));
     g_stats.frame_count = e.frame_count;
     pthread_mutex_unlock(&g_stats_mu);
-    buf_t *outs = (buf_t *)calloc((size_t)e.frame_count, sizeof(buf_t));
+    buf_t *outs = (buf_t *)calloc((size_t)(e.frame_count > 0 ? e.frame_count : 1), sizeof(buf_t));
+    int nf = frame_end - frame_begin;
     if (threads <= 0) threads = 1;
-    if (threads > e.frame_count) threads = e.frame_count;
+    if (threads > nf) threads = nf;
     pool_t pl;
     pl.e = &e;
     pl.outs = outs;
-    pl.next = 0;
+    pl.next = frame_begin;
+    pl.end = frame_end;
     pthread_mutex_init(&pl.mu, NULL);
     if (threads <= 1) {
         worker(&pl);
@@ -862,15 +872,20 @@ int ora_encode(const uint8_t *wav, size_t wav_len, const gsc_params *p, int thre
     }
     pthread_mutex_destroy(&pl.mu);
     buf_t all = {0};
-    for (int i = 0; i < e.frame_count; i++) {
+    for (int i = frame_begin; i < frame_end; i++) {
         put(&all, outs[i].b, outs[i].n);
         free(outs[i].b);
     }
     free(outs);
     enc_free(&e);
+    if (!all.b) all.b = (uint8_t *)malloc(1);
     *out = all.b;
     *out_len = all.n;
     return 0;
+}
+
+int ora_encode(const uint8_t *wav, size_t wav_len, const gsc_params *p, int threads, uint8_t **out, size_t *out_len) {
+    return ora_encode_frames(wav, wav_len, p, 0, -1, threads, out, out_len, NULL);
 }
 
 int ora_trace_frame(const uint8_t *wav, size_t wav_len, const gsc_params *p, int frame_idx, ora_frame_trace *tr) {

@@ -53,6 +53,10 @@ void ora_parse_params(gsc_params *p, int argc, const char *const *argv);
 int ora_encode(const uint8_t *wav, size_t wav_len, const gsc_params *p, int threads, uint8_t **out,
                size_t *out_len);
 void ora_free(void *p);
+/* Frames [frame_begin, frame_end) only (frame_end < 0 => all), concatenated
+ * SaveStream bytes; *frame_count (may be NULL) = frames in the file. */
+int ora_encode_frames(const uint8_t *wav, size_t wav_len, const gsc_params *p, int frame_begin, int frame_end,
+                      int threads, uint8_t **out, size_t *out_len, int *frame_count);
 
 /* Statistics of the last ora_encode (process-global, for tests/bench). */
 typedef struct {

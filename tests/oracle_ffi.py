@@ -60,6 +60,10 @@ def load():
         lib.ora_encode.argtypes = [u8p, ctypes.c_size_t, ctypes.POINTER(OraParams), ctypes.c_int,
                                    ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]
         lib.ora_encode.restype = ctypes.c_int
+        lib.ora_encode_frames.argtypes = [u8p, ctypes.c_size_t, ctypes.POINTER(OraParams), ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t),
+                                          ctypes.POINTER(ctypes.c_int)]
+        lib.ora_encode_frames.restype = ctypes.c_int
         lib.ora_free.argtypes = [ctypes.c_void_p]
         lib.ora_get_stats.argtypes = [ctypes.POINTER(OraStats)]
         lib.ora_trace_frame.argtypes = [u8p, ctypes.c_size_t, ctypes.POINTER(OraParams), ctypes.c_int,
@@ -110,6 +114,24 @@ def encode(wav: bytes, argv=(), threads: int = 1) -> bytes:
         raise RuntimeError(f"oracle encode failed: {rc}")
     try:
         return ctypes.string_at(out, n.value)
+    finally:
+        lib.ora_free(out)
+
+
+def encode_frames(wav: bytes, argv=(), frame_begin: int = 0, frame_end: int = -1, threads: int = 1):
+    """Frames [frame_begin, frame_end) -> (bytes, total frame count)."""
+    lib = load()
+    p = params(argv)
+    a, ptr = _u8(wav)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t(0)
+    fc = ctypes.c_int(0)
+    rc = lib.ora_encode_frames(ptr, len(a), ctypes.byref(p), frame_begin, frame_end, threads, ctypes.byref(out),
+                               ctypes.byref(n), ctypes.byref(fc))
+    if rc != 0:
+        raise RuntimeError(f"oracle encode failed: {rc}")
+    try:
+        return ctypes.string_at(out, n.value), fc.value
     finally:
         lib.ora_free(out)
 

@@ -1,0 +1,141 @@
+"""Oracle regression against the committed golden .gsc fixtures, .gsc format
+checks through the decoder restatement (decoder/decoder.lpr:37-220), and the
+ANN / yakmo restatements against brute force where their semantics are
+exactly known (fresh tree => exact nearest neighbour, first-visited minimum).
+
+Pinning: the golden .gsc files were produced by this oracle
+(tests/golden/make_golden.py); the reference ships no .gsc and its encoder
+cannot run here, so whole-file parity with the reference is
+unpinned beyond the quantiser KAT and the decoder round trip.
+"""
+from __future__ import annotations
+
+import ctypes
+import struct
+
+import numpy as np
+import pytest
+
+import oracle_ffi
+from golden.cases import CASES, golden_path
+
+FAST = ["tiny_passthrough_cs8", "silence_tone_cs8_cpf256", "hihat_cs8_cpf256", "hihat_cs4_default"]
+
+
+@pytest.mark.parametrize("name", FAST)
+def test_oracle_reproduces_golden(name):
+    make, argv = CASES[name]
+    assert oracle_ffi.encode(make(), argv, threads=4) == golden_path(name).read_bytes()
+
+
+def _frame_headers(gsc: bytes):
+    """Walk TFrame.SaveStream headers (encoder.lpr:988-1106 / SURVEY App. B)."""
+    pos, out = 0, []
+    while pos < len(gsc):
+        ver, ch = gsc[pos], gsc[pos + 1]
+        kw, = struct.unpack_from("<H", gsc, pos + 2)
+        bd, cs = gsc[pos + 4], gsc[pos + 5]
+        sr, = struct.unpack_from("<I", gsc, pos + 6)
+        div, = struct.unpack_from("<H", gsc, pos + 10)
+        out.append(dict(ver=ver, ch=ch, K=kw & 0x1FFF, bd=bd, cs=cs, sr=sr & 0xFFFFFF, div=div))
+        return out  # first frame is enough for header checks
+    return out
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_golden_decodes(name):
+    make, argv = CASES[name]
+    wav = make()
+    gsc = golden_path(name).read_bytes()
+    ch = struct.unpack_from("<H", wav, 22)[0]
+    rate = struct.unpack_from("<I", wav, 24)[0]
+    h = _frame_headers(gsc)[0]
+    assert h["ver"] == 1 and h["ch"] == ch and h["sr"] == rate
+    assert 1 <= h["div"] <= 64
+    cs = int(next((a[3:] for a in argv if a.startswith("-cs")), "4"))
+    assert h["cs"] == cs
+    pcm, dch, drate = oracle_ffi.decode(gsc)
+    assert dch == ch and drate == rate
+    n_in = (len(wav) - 44) // 2
+    # the encoder pads the sample count to a ChunkSize multiple (encoder.lpr:1318-1323)
+    assert n_in <= pcm.size < n_in + cs * ch + 1
+    src = np.frombuffer(wav[44:44 + 2 * n_in], dtype="<i2").astype(np.float64)
+    dec = pcm[:n_in].astype(np.float64)
+    if np.abs(src).max() > 1000:
+        # vector quantisation keeps the waveform: clearly positive correlation
+        c = np.corrcoef(src, dec)[0, 1]
+        assert c > 0.5, c
+
+
+def _ann(lib):
+    fp = ctypes.POINTER(ctypes.c_float)
+    lib.ora_kdtree_create.argtypes = [ctypes.POINTER(fp), ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.ora_kdtree_create.restype = ctypes.c_void_p
+    lib.ora_kdtree_destroy.argtypes = [ctypes.c_void_p]
+    lib.ora_kdtree_search.argtypes = [ctypes.c_void_p, fp, ctypes.c_float, fp]
+    lib.ora_kdtree_search.restype = ctypes.c_int
+    lib.ora_kdtree_pri_search_multi.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), fp, ctypes.c_int, fp,
+                                                ctypes.c_float]
+    return lib
+
+
+def _rows(a):
+    fp = ctypes.POINTER(ctypes.c_float)
+    rows = (fp * a.shape[0])(*[a[i].ctypes.data_as(fp) for i in range(a.shape[0])])
+    return rows
+
+
+def _seq_dist(p, q):
+    d = np.float32(0)
+    for k in range(p.shape[0]):
+        t = np.float32(q[k] - p[k])
+        d = np.float32(d + np.float32(t * t))
+    return d
+
+
+@pytest.mark.parametrize("n,dd", [(1, 4), (7, 3), (256, 16), (1000, 8)])
+def test_ann_fresh_tree_is_exact_nn(n, dd):
+    lib = _ann(oracle_ffi.load())
+    rng = np.random.default_rng(n * 31 + dd)
+    pts = rng.standard_normal((n, dd)).astype(np.float32)
+    pts[n // 2:] = np.round(pts[n // 2:] * 4) / 4  # duplicates / exact ties
+    rows = _rows(pts)
+    t = lib.ora_kdtree_create(rows, n, dd, 1)
+    fp = ctypes.POINTER(ctypes.c_float)
+    try:
+        for _ in range(200):
+            q = (rng.standard_normal(dd) * 1.2).astype(np.float32)
+            err = ctypes.c_float(0)
+            idx = lib.ora_kdtree_search(t, q.ctypes.data_as(fp), 0.0, ctypes.byref(err))
+            d = np.array([_seq_dist(p, q) for p in pts], dtype=np.float32)
+            assert err.value == d.min() and d[idx] == d.min()
+            k = min(8, n)
+            idxs = np.zeros(k, np.int32)
+            errs = np.zeros(k, np.float32)
+            lib.ora_kdtree_pri_search_multi(t, idxs.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                            errs.ctypes.data_as(fp), k, q.ctypes.data_as(fp), 0.0)
+            np.testing.assert_array_equal(errs, np.sort(d)[:k])
+    finally:
+        lib.ora_kdtree_destroy(t)
+
+
+def test_yakmo_seed_means_properties():
+    lib = oracle_ffi.load()
+    fp = ctypes.POINTER(ctypes.c_float)
+    rng = np.random.default_rng(3)
+    N, D, K = 600, 8, 16
+    x = rng.standard_normal((N, D)).astype(np.float32)
+    c = np.zeros((K, D), np.float32)
+    lab = np.zeros(N, np.int32)
+    assert lib.ora_yakmo_seed_means(N, D, x.ctypes.data_as(fp), K, c.ctypes.data_as(fp),
+                                    lab.ctypes.data_as(ctypes.POINTER(ctypes.c_int))) == 0
+    # every centroid is the f32 mean (in point order) of its seeding cluster
+    for k in range(K):
+        m = x[lab == k]
+        s = np.zeros(D, np.float32)
+        for row in m:
+            s = (s + row).astype(np.float32)
+        np.testing.assert_array_equal(c[k], (s / np.float32(len(m))).astype(np.float32))
+    # K >= N is rejected (the DLL would spin)
+    assert lib.ora_yakmo_seed_means(4, D, x.ctypes.data_as(fp), 4, c.ctypes.data_as(fp),
+                                    lab.ctypes.data_as(ctypes.POINTER(ctypes.c_int))) == -1
