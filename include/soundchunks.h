@@ -111,6 +111,7 @@ typedef struct {
     long long scan_point_passes; /* sum over frames of passes * N (searches) */
     long long knnfit_pairs;      /* sum over frames of N * 4R (query x candidate) */
     int scan_launches, knnfit_launches;
+    long long scan_restarts;     /* batched KNNScanReduce pipeline restarts */
 } gsc_timing;
 void gsc_last_timing(gsc_timing *t);
 

@@ -282,7 +282,7 @@ void ora_sort_count_desc(int n, const int *counts, int *perm) {
 }
 
 /* ---- KNNScanReduce (encoder.lpr:699-765) -------------------------------- */
-int ora_scan_reduce(int N, int D, const float *X, int K, float *C, int *clusters, int precision) {
+int ora_scan_reduce_n(int N, int D, const float *X, int K, float *C, int *clusters, int precision, int max_passes) {
     float **rows = (float **)malloc(sizeof(float *) * (size_t)K);
     for (int j = 0; j < K; j++) rows[j] = C + (size_t)j * D;
     int *cnts[2];
@@ -322,7 +322,7 @@ int ora_scan_reduce(int N, int D, const float *X, int K, float *C, int *clusters
         iter++;
         ora_kdtree_destroy(kdt);
         double diff = err > prev_err ? err - prev_err : prev_err - err;
-        if (diff <= tol || iter >= 100) break;
+        if (diff <= tol || iter >= max_passes) break;
     }
     pthread_mutex_lock(&g_stats_mu);
     g_stats.scan_iterations += iter;
@@ -334,6 +334,10 @@ int ora_scan_reduce(int N, int D, const float *X, int K, float *C, int *clusters
     free(cnts[0]);
     free(cnts[1]);
     return iter;
+}
+
+int ora_scan_reduce(int N, int D, const float *X, int K, float *C, int *clusters, int precision) {
+    return ora_scan_reduce_n(N, D, X, K, C, clusters, precision, 100);
 }
 
 /* ---- KNNFit core (encoder.lpr:945-965) --------------------------------- */

@@ -86,6 +86,8 @@ void ora_chunk_features(int cs, const double *src, int neg, int rev, double *dct
 /* KNNScanReduce (encoder.lpr:699-765) on row-major X[N][D], C[K][D] in/out.
  * Returns the number of passes. */
 int ora_scan_reduce(int N, int D, const float *X, int K, float *C, int *clusters, int precision);
+/* same, stopping after at most max_passes passes (stage-level tests) */
+int ora_scan_reduce_n(int N, int D, const float *X, int K, float *C, int *clusters, int precision, int max_passes);
 
 /* KNNFit core (encoder.lpr:940-965): candidates cand[4R][CS] (already built),
  * queries q[N][CS] f32; writes best candidate index per query. */

@@ -52,6 +52,7 @@ class GscTiming(ctypes.Structure):
         ("knnfit_pairs", ctypes.c_longlong),
         ("scan_launches", ctypes.c_int),
         ("knnfit_launches", ctypes.c_int),
+        ("scan_restarts", ctypes.c_longlong),
     ]
 
 
@@ -104,7 +105,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path is not None else LIB_PATH
+    p = Path(path) if path is not None else Path(os.environ.get("GSC_LIB", LIB_PATH))
     if not p.exists():
         raise GscError(f"{p} not built; run __graft_entry__.build() or make -C soundchunks_amd/csrc")
     lib = ctypes.CDLL(str(p))

@@ -8,6 +8,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -25,7 +26,10 @@ extern "C" hipError_t gsc_launch_yakmo(int D, const gsc::ReduceFrame* frames, in
                                        float* fs, int* is, uint32_t* bits, hipStream_t st);
 extern "C" hipError_t gsc_launch_scan_pass(int D, gsc::ReduceFrame* frames, int nframes, int K, const float* X,
                                            float* C, int* is, float* fs, const float* rate_tab, double tol, int pass,
-                                           hipStream_t st);
+                                           int only_flagged, hipStream_t st);
+extern "C" hipError_t gsc_launch_scan_batch(int D, int logk, gsc::ReduceFrame* frames, int nframes, const float* X,
+                                            float* C, int* is, const float* rate_tab, double tol, int pass,
+                                            hipStream_t st);
 extern "C" hipError_t gsc_launch_knnfit(int CS, gsc::FitFrame* frames, int nframes, int max_n, int max_r,
                                         const float* cand, const float* q, int* out, hipStream_t st);
 
@@ -135,12 +139,30 @@ double scan_tolerance(int precision) {
     return 1.0 / p;
 }
 
-// all KNNScanReduce passes of a batch: one launch per pass, converged frames exit early
+// K = 2^logk in [256, 4096] and D in {8, 16}: the batched speculative kernel
+// (gsc_scan.hip) covers the pass; anything else runs the generic kernel.
+bool batched_scan_shape(int D, int K) {
+    if (std::getenv("GSC_SCAN_GENERIC")) return false;  // diagnostic switch
+    return (D == 8 || D == 16) && K >= 256 && K <= 4096 && (K & (K - 1)) == 0;
+}
+
+// all KNNScanReduce passes of a batch: one launch per pass, converged frames
+// exit early; the generic launch after a batched one only runs the frames the
+// batched kernel handed over (NaN centroids)
 hipError_t launch_scan_passes(int D, ReduceFrame* dfr, int nf, int K, const float* X, float* C, int* is, float* fs,
                               const float* rate, int precision) {
     const double tol = scan_tolerance(precision);
-    for (int pass = 0; pass < kMaxScanIters; ++pass) {
-        const hipError_t e = gsc_launch_scan_pass(D, dfr, nf, K, X, C, is, fs, rate, tol, pass, nullptr);
+    const bool batched = batched_scan_shape(D, K);
+    int logk = 0;
+    while ((1 << logk) < K) ++logk;
+    int max_passes = kMaxScanIters;
+    if (const char* e = std::getenv("GSC_SCAN_MAX_PASSES")) max_passes = std::max(1, std::min(kMaxScanIters, std::atoi(e)));
+    for (int pass = 0; pass < max_passes; ++pass) {
+        if (batched) {
+            const hipError_t e = gsc_launch_scan_batch(D, logk, dfr, nf, X, C, is, rate, tol, pass, nullptr);
+            if (e != hipSuccess) return e;
+        }
+        const hipError_t e = gsc_launch_scan_pass(D, dfr, nf, K, X, C, is, fs, rate, tol, pass, batched ? 1 : 0, nullptr);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -160,7 +182,7 @@ std::vector<float> rate_table(int n) {
 // are concatenated per frame (N_f*D and K*D floats).
 int run_reduce_batch(int D, int K, int precision, const std::vector<int>& Ns, const std::vector<float>& X,
                      std::vector<float>* C, std::vector<int>* clusters, std::vector<int>* iters, std::vector<int>* slow,
-                     double* yakmo_ms, double* scan_ms) {
+                     long long* restarts, double* yakmo_ms, double* scan_ms) {
     // launches: one yakmo launch + kMaxScanIters scan launches per batch
     const int nf = int(Ns.size());
     if (nf == 0) return 0;
@@ -223,6 +245,8 @@ int run_reduce_batch(int D, int K, int precision, const std::vector<int>& Ns, co
     for (int i = 0; i < nf; ++i) {
         (*iters)[i] = fr[i].iters;
         (*slow)[i] = fr[i].slow;
+        if (restarts) *restarts += fr[i].restarts;
+        if (fr[i].loop_iters < 0) return fail("KNNScanReduce: batched pipeline made no progress (guard tripped)");
     }
     return 0;
 }
@@ -309,7 +333,7 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
             Ns.push_back(frames[i].n);
         }
     double yak_ms = 0, scan_ms = 0, knn_ms = 0;
-    long long passes = 0, slow = 0;
+    long long passes = 0, slow = 0, restarts = 0;
     if (!red_idx.empty()) {
         std::vector<float> X;
         size_t tot = 0;
@@ -318,7 +342,7 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
         for (int i : red_idx) X.insert(X.end(), frames[i].feat.begin(), frames[i].feat.end());
         std::vector<float> C;
         std::vector<int> cl, it, sl;
-        if (run_reduce_batch(D, K, opt_.precision, Ns, X, &C, &cl, &it, &sl, &yak_ms, &scan_ms) != 0) {
+        if (run_reduce_batch(D, K, opt_.precision, Ns, X, &C, &cl, &it, &sl, &restarts, &yak_ms, &scan_ms) != 0) {
             *err = t_err;
             return -1;
         }
@@ -398,6 +422,7 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
         tim->points = pts;
         tim->scan_passes = passes;
         tim->scan_slow = slow;
+        tim->scan_restarts = restarts;
         long long pp = 0;
         for (auto& f : frames) pp += (long long)f.scan_iters * f.n;
         tim->scan_point_passes = pp;
@@ -573,6 +598,17 @@ int gsc_scan_reduce(int n, int d, const float* x, int k, float* centroids, int* 
     HIP_TRY(hipMemcpy(clusters, dI.p, sizeof(int) * size_t(n), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(fr.data(), dFr.p, sizeof(ReduceFrame), hipMemcpyDeviceToHost));
     if (iters) *iters = fr[0].iters;
+    if (fr[0].loop_iters < 0) return fail("KNNScanReduce: batched pipeline made no progress (guard tripped)");
+    if (std::getenv("GSC_SCAN_DEBUG"))
+    {
+        std::fprintf(stderr, "scan: passes %d slow %d restarts %d loop_iters(last pass) %d err %.9g\n", fr[0].iters,
+                     fr[0].slow, fr[0].restarts, fr[0].loop_iters, fr[0].err);
+        std::fprintf(stderr, "stamps w0 [S A1 B1 A2 B2 refresh]:");
+        for (int k = 0; k < 6; ++k) std::fprintf(stderr, " %.3g", double(fr[0].stamps[k]));
+        std::fprintf(stderr, "\nstamps w1:");
+        for (int k = 6; k < 12; ++k) std::fprintf(stderr, " %.3g", double(fr[0].stamps[k]));
+        std::fprintf(stderr, "\n");
+    }
     return 0;
 }
 

@@ -1,0 +1,308 @@
+// Shared device code of the KNNScanReduce kernels (gsc_kernels.hip: generic
+// per-search kernel; gsc_scan.hip: batched speculative kernel).
+//
+//   KdTree          ANN_KD_STD kd-tree (bs = 1) over the centroids of one
+//                   pass, in LDS, heap-indexed (root 0, children 2h+1 / 2h+2).
+//   build_tree      annMaxSpread + annMedianSplit level by level
+//                   (ANN.dll @0x180015260, @0x180015680).
+//   scan_exact_dfs  ANN's k = 1 standard search (annkSearch @0x1800124b0)
+//                   over precomputed live leaf distances (stale tree).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <stdint.h>
+
+#include "gsc_device.h"
+
+namespace gsc {
+
+__device__ __forceinline__ float fadd(float a, float b) { return __fadd_rn(a, b); }
+__device__ __forceinline__ float fsub(float a, float b) { return __fsub_rn(a, b); }
+__device__ __forceinline__ float fmul(float a, float b) { return __fmul_rn(a, b); }
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+template <typename T>
+__device__ __forceinline__ T ld_relaxed(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct KdTree {
+    float cv[kMaxInternal + 1];    // cut value per split node
+    float lo[kMaxInternal + 1];    // cd_bnds lo / hi of the split node's cell
+    float hi[kMaxInternal + 1];
+    uint16_t pidx[kMaxK];          // kd-leaf position -> centroid id
+    uint8_t cd[kMaxInternal + 1];  // cut dimension
+    float bnd_lo[32], bnd_hi[32];  // annEnclRect of the pass's centroids
+};
+
+// segment of heap node h (root 0, children 2h+1 / 2h+2, n_lo = n/2)
+__device__ __forceinline__ void node_segment(int h, int K, int& s, int& n, int& depth) {
+    s = 0;
+    n = K;
+    depth = 0;
+    int path = h + 1;
+    int lvl = 31 - __clz(path);
+    depth = lvl;
+    for (int l = lvl - 1; l >= 0; --l) {
+        const int half = n >> 1;
+        if ((path >> l) & 1) {
+            s += half;
+            n -= half;
+        } else {
+            n = half;
+        }
+    }
+}
+
+template <int D>
+__device__ void build_tree(KdTree& sh, float* __restrict__ scratch, const float* __restrict__ C, int K) {
+    const int tid = threadIdx.x;
+    const int nthr = blockDim.x;
+    for (int p = tid; p < K; p += nthr) sh.pidx[p] = (uint16_t)p;
+    // annEnclRect: sequential min/max from PA(0,d); NaNs never win a compare
+    if (tid < D) {
+        const int d = tid;
+        float lo = C[d], hi = C[d];
+        for (int i = 0; i < K; ++i) {
+            const float v = C[(int64_t)i * D + d];
+            if (v < lo) lo = v;
+            else if (v > hi) hi = v;
+        }
+        sh.bnd_lo[d] = lo;
+        sh.bnd_hi[d] = hi;
+    }
+    __syncthreads();
+    // split level by level; one thread per node runs ANN's exact sequential code
+    for (int level = 0; level < 12; ++level) {
+        const int first = (1 << level) - 1;
+        const int count = 1 << level;
+        for (int j = tid; j < count; j += nthr) {
+            const int h = first + j;
+            if (h > kMaxInternal - 1) continue;
+            int s, n, depth;
+            node_segment(h, K, s, n, depth);
+            if (n < 2) continue;
+            uint16_t* pidx = sh.pidx + s;
+            // annMaxSpread: first dim with strictly largest spread
+            int cdim = 0;
+            float max_spr = 0.0f;
+            {
+                float mn[D], mx[D];
+                const float* p0 = C + (int64_t)pidx[0] * D;
+#pragma unroll
+                for (int d = 0; d < D; ++d) mn[d] = mx[d] = p0[d];
+                for (int i = 1; i < n; ++i) {
+                    const float* pp = C + (int64_t)pidx[i] * D;
+#pragma unroll
+                    for (int d = 0; d < D; ++d) {
+                        const float c = pp[d];
+                        if (c < mn[d]) mn[d] = c;
+                        else if (c > mx[d]) mx[d] = c;
+                    }
+                }
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    const float spr = fsub(mx[d], mn[d]);
+                    if (spr > max_spr) {
+                        max_spr = spr;
+                        cdim = d;
+                    }
+                }
+            }
+            float* val = scratch + s;  // cut-dim values of the segment
+            for (int i = 0; i < n; ++i) val[i] = C[(int64_t)pidx[i] * D + cdim];
+            const int n_lo = n >> 1;
+            // annMedianSplit (ANN.dll @0x180015680)
+            int l = 0, r = n - 1;
+#define PSWAP(a, b)                 \
+    {                               \
+        const uint16_t t_ = pidx[a]; \
+        pidx[a] = pidx[b];          \
+        pidx[b] = t_;               \
+        const float v_ = val[a];    \
+        val[a] = val[b];            \
+        val[b] = v_;                \
+    }
+            while (l < r) {
+                int i = (r + l) / 2;
+                int k;
+                if (val[i] > val[r]) PSWAP(i, r)
+                PSWAP(l, i);
+                const float c = val[l];
+                i = l;
+                k = r;
+                for (;;) {
+                    while (val[++i] < c) {}
+                    while (val[--k] > c) {}
+                    if (i < k) PSWAP(i, k) else break;
+                }
+                PSWAP(l, k);
+                if (k > n_lo) r = k - 1;
+                else if (k < n_lo) l = k + 1;
+                else break;
+            }
+            if (n_lo > 0) {
+                float c = val[0];
+                int k = 0;
+                for (int i = 1; i < n_lo; ++i)
+                    if (val[i] > c) {
+                        c = val[i];
+                        k = i;
+                    }
+                PSWAP(n_lo - 1, k);
+            }
+#undef PSWAP
+            const float cvv = (float)((double)fadd(val[n_lo - 1], val[n_lo]) / 2.0);
+            // node bounds: root rect narrowed by ancestors cutting the same dim
+            float lov = sh.bnd_lo[cdim], hiv = sh.bnd_hi[cdim];
+            {
+                int a = 0;
+                const int path = h + 1;
+                for (int bl = depth - 1; bl >= 0; --bl) {
+                    const int right = (path >> bl) & 1;
+                    if (sh.cd[a] == cdim) {
+                        if (right) lov = sh.cv[a];
+                        else hiv = sh.cv[a];
+                    }
+                    a = 2 * a + 1 + right;
+                }
+            }
+            sh.cd[h] = (uint8_t)cdim;
+            sh.cv[h] = cvv;
+            sh.lo[h] = lov;
+            sh.hi[h] = hiv;
+        }
+        __syncthreads();
+    }
+}
+
+// depth of the lowest common ancestor of kd-leaf positions p and q (p != q)
+__device__ __forceinline__ int lca_depth(int p, int q, int K, int log2K, bool pow2) {
+    if (pow2) return __clz(p ^ q) - (32 - log2K);
+    int s = 0, n = K, depth = 0;
+    for (;;) {
+        const int half = n >> 1;
+        const bool a = p >= s + half, b = q >= s + half;
+        if (a != b) return depth;
+        if (a) {
+            s += half;
+            n -= half;
+        } else {
+            n = half;
+        }
+        ++depth;
+    }
+}
+
+// Exact ANN ann_search (k = 1, eps = 0) over the stale tree with the live
+// distances already in dist[].  Single lane.  For a NaN leaf visited while
+// the result list is still empty, ANN's early exit depends on the partial sum
+// before the first NaN term; that is recomputed from the live mirror in C.
+template <int D>
+__device__ __noinline__ void scan_exact_dfs(const KdTree& sh, const float* __restrict__ dist, const float (&q)[D], int K,
+                                            const float* __restrict__ C, int& out_pos, float& out_key) {
+    int st_h[16], st_s[16], st_n[16];
+    float st_box[16];
+    int sp = 0, nmk = 0, best = -1;
+    float key = FLT_MAX;
+    float cur_box = 0.0f;
+    for (int d = 0; d < D; ++d) {
+        if (q[d] < sh.bnd_lo[d]) {
+            const float t = fsub(sh.bnd_lo[d], q[d]);
+            cur_box = fadd(cur_box, fmul(t, t));
+        } else if (q[d] > sh.bnd_hi[d]) {
+            const float t = fsub(q[d], sh.bnd_hi[d]);
+            cur_box = fadd(cur_box, fmul(t, t));
+        }
+    }
+    int h = 0, s = 0, n = K;
+    for (;;) {
+        if (n == 1) {
+            // ANNkd_leaf::ann_search: skipped iff some partial sum exceeds min_dist
+            const float dd = dist[s];
+            const float min_dist = nmk == 1 ? key : FLT_MAX;
+            float chk = dd;
+            if (dd != dd) {
+                const float* c = C + (int64_t)sh.pidx[s] * D;
+                float pr = 0.0f;
+                for (int d = 0; d < D; ++d) {
+                    const float t = fsub(q[d], c[d]);
+                    const float sq = fmul(t, t);
+                    if (sq != sq) break;
+                    pr = fadd(pr, sq);
+                }
+                chk = pr;
+            }
+            if (!(chk > min_dist)) {
+                if (nmk == 0) {
+                    key = dd;
+                    best = s;
+                    nmk = 1;
+                } else if (key > dd) {
+                    key = dd;
+                    best = s;
+                }
+            }
+            // return up the recursion: far child visited iff box' < max_key
+            bool found = false;
+            while (sp > 0) {
+                --sp;
+                const float mk = nmk == 1 ? key : FLT_MAX;
+                if ((double)st_box[sp] < (double)mk) {
+                    h = st_h[sp];
+                    s = st_s[sp];
+                    n = st_n[sp];
+                    cur_box = st_box[sp];
+                    found = true;
+                    break;
+                }
+            }
+            if (!found) break;
+            continue;
+        }
+        // ANNkd_split::ann_search: descend near child, remember far child + box'
+        const int half = n >> 1;
+        const int cdim = sh.cd[h];
+        const float qc = q[cdim];
+        const float cut = fsub(qc, sh.cv[h]);
+        float bd;
+        int nh, ns, nn;
+        if (cut < 0.0f) {
+            bd = fsub(sh.lo[h], qc);
+            nh = 2 * h + 1;
+            ns = s;
+            nn = half;
+            st_h[sp] = 2 * h + 2;
+            st_s[sp] = s + half;
+            st_n[sp] = n - half;
+        } else {
+            bd = fsub(qc, sh.hi[h]);
+            nh = 2 * h + 2;
+            ns = s + half;
+            nn = n - half;
+            st_h[sp] = 2 * h + 1;
+            st_s[sp] = s;
+            st_n[sp] = half;
+        }
+        if (bd < 0.0f) bd = 0.0f;
+        st_box[sp] = fadd(cur_box, fsub(fmul(cut, cut), fmul(bd, bd)));
+        ++sp;
+        h = nh;
+        s = ns;
+        n = nn;
+    }
+    out_pos = best;
+    out_key = key;
+}
+
+template <typename T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (T*)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int uniform_int(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+}  // namespace gsc

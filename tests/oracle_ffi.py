@@ -84,6 +84,8 @@ def load():
         ip = ctypes.POINTER(ctypes.c_int)
         lib.ora_yakmo_seed_means.argtypes = [ctypes.c_int, ctypes.c_int, fp, ctypes.c_int, fp, ip]
         lib.ora_scan_reduce.argtypes = [ctypes.c_int, ctypes.c_int, fp, ctypes.c_int, fp, ip, ctypes.c_int]
+        lib.ora_scan_reduce_n.argtypes = [ctypes.c_int, ctypes.c_int, fp, ctypes.c_int, fp, ip, ctypes.c_int,
+                                          ctypes.c_int]
         lib.ora_knnfit_assign.argtypes = [ctypes.c_int, ctypes.c_int, fp, ctypes.c_int, fp, ctypes.c_float, ip]
         _lib = lib
     return _lib
@@ -134,6 +136,17 @@ def encode_frames(wav: bytes, argv=(), frame_begin: int = 0, frame_end: int = -1
         return ctypes.string_at(out, n.value), fc.value
     finally:
         lib.ora_free(out)
+
+
+def scan_reduce(x, c0, precision=3, max_passes=100):
+    """KNNScanReduce restatement: (centroids, clusters, passes)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    c = np.ascontiguousarray(c0, dtype=np.float32).copy()
+    cl = np.zeros(x.shape[0], dtype=np.int32)
+    fp, ip = ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)
+    n = load().ora_scan_reduce_n(x.shape[0], x.shape[1], x.ctypes.data_as(fp), c.shape[0], c.ctypes.data_as(fp),
+                                 cl.ctypes.data_as(ip), precision, max_passes)
+    return c, cl, n
 
 
 def stats() -> dict:
