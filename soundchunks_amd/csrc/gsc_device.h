@@ -19,7 +19,8 @@ struct ReduceFrame {
     int64_t x_off;        // Dataset: N*D floats at X + x_off (row major)
     int64_t c_off;        // Centroids: K*D floats at C + c_off (yakmo out, scan in/out)
     int64_t n_off;        // per-point scratch (N): clusters, d0, id, cum at +n_off
-    int64_t k_off;        // per-centroid scratch (K): counts
+    int64_t k_off;        // per-centroid scratch (K): previous-pass counts by centroid id
+    int64_t ka_off;       // per-centroid scratch (K): this pass's counts by kd-leaf position
     int32_t N, K;
     int32_t iters;        // out: KNNScanReduce passes
     int32_t slow;         // out: searches resolved by the exact DFS fallback

@@ -201,7 +201,10 @@ int run_reduce_batch(int D, int K, int precision, const std::vector<int>& Ns, co
         no += Ns[i];
         maxN = std::max<int64_t>(maxN, Ns[i]);
     }
-    for (int i = 0; i < nf; ++i) fr[i].k_off = no + int64_t(i) * K;
+    for (int i = 0; i < nf; ++i) {
+        fr[i].k_off = no + int64_t(i) * K;
+        fr[i].ka_off = no + int64_t(nf + i) * K;
+    }
     DevBuf<float> dX, dC, dF, dRate;
     DevBuf<int> dI;
     DevBuf<uint32_t> dBits;
@@ -209,7 +212,7 @@ int run_reduce_batch(int D, int K, int precision, const std::vector<int>& Ns, co
     HIP_TRY(dX.alloc(size_t(xo)));
     HIP_TRY(dC.alloc(size_t(nf) * K * D));
     HIP_TRY(dF.alloc(size_t(no) * 3));
-    HIP_TRY(dI.alloc(size_t(no) + size_t(nf) * K));
+    HIP_TRY(dI.alloc(size_t(no) + 2 * size_t(nf) * K));
     HIP_TRY(dBits.alloc(size_t(no / 32) + size_t(nf) * 2 + 2));
     HIP_TRY(dFr.alloc(size_t(nf)));
     const std::vector<float> rt = rate_table(int(maxN));
@@ -578,13 +581,14 @@ int gsc_scan_reduce(int n, int d, const float* x, int k, float* centroids, int* 
     fr[0].N = n;
     fr[0].K = k;
     fr[0].k_off = n;
+    fr[0].ka_off = n + k;
     DevBuf<float> dX, dC, dRate, dF;
     DevBuf<int> dI;
     DevBuf<ReduceFrame> dFr;
     HIP_TRY(dF.alloc(size_t(n) * 3));
     HIP_TRY(dX.alloc(size_t(n) * d));
     HIP_TRY(dC.alloc(size_t(k) * d));
-    HIP_TRY(dI.alloc(size_t(n) + size_t(k)));
+    HIP_TRY(dI.alloc(size_t(n) + 2 * size_t(k)));
     HIP_TRY(dFr.alloc(1));
     const std::vector<float> rt = rate_table(n);
     HIP_TRY(dRate.alloc(rt.size()));

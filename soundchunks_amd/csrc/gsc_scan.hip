@@ -14,35 +14,43 @@
 // position p = (wave*64 + lane)*8 + slot and every kd subtree is an aligned
 // block of waves / lanes / slots.
 //
-// Pipeline, per iteration (batches of kBatch queries):
-//   S  (wave 0)   serial commit of the PREVIOUS batch: for each query, check
-//                 its speculative answer against the update log (the <= 64
-//                 centroids moved since the snapshot its distances were
-//                 computed on), then apply the online update to the log.
-//   A1 (all)      snapshot distances of the CURRENT batch: every lane computes
-//                 its 8 leaf distances (bit-exact sequential f32, no FMA), and
-//                 a wave min-tree (DPP) yields per wave: min, tie flag, argmin
-//                 position and the min of every sibling subtree on the path
-//                 to that argmin.
-//   A2 (all)      per query: global argmin c*, the ANN DFS certificate on c*'s
-//                 root path (box' of every far step vs the min of the sibling
-//                 subtree visited before it), second minimum m2.
-//   refresh       owners fold the log into their registers.
-// A query whose certificate or log check fails restarts the pipeline at that
-// query with a fresh snapshot; if it fails on a fresh snapshot it is resolved
-// by the exact single-lane DFS (scan_exact_dfs) over live distances.
+// Pipeline, per iteration (batches of kBatch queries; "current" = the batch
+// whose distances are computed now, "pending" = the previous batch, whose
+// speculative answers are committed now):
+//   part 1  A1 (all waves): snapshot distances of the current batch: each lane
+//           computes its 8 leaf distances (bit-exact sequential f32, no FMA);
+//           a wave min-tree (DPP) gives per wave the minimum, a tie flag, the
+//           argmin position and the minimum of every sibling subtree on the
+//           path to it.  Wave 0 first chains the pending batch's online
+//           updates (c += (x - c) * rate per query, in order per centroid).
+//   part 2  V (all waves): every pending query is checked against every
+//           centroid moved since its snapshot (the update log + the earlier
+//           queries of its batch), with live coordinates.
+//           A2 (all waves, 4 queries per wave): ANN DFS certificate of the
+//           current batch: global argmin c*, box' of every far step on c*'s
+//           root path against the minimum of the sibling subtree visited
+//           before it, second minimum m2.
+//   part 3  commit the valid prefix of the pending batch (clusters, counts,
+//           residual in order, update log), choose the next batch.
+//   part 4  owners fold the log into their registers.
+// A query that fails restarts the pipeline at that query on a fresh snapshot;
+// if it fails on a fresh snapshot it is resolved by the exact single-lane DFS
+// (dfs_exact) over live distances.
 //
 // Certificate (why c* is ANN's answer): c* is the unique global minimum; ANN
 // visits c* iff at every far step u on c*'s root path box'(u) < best-so-far;
 // best-so-far there is a minimum over leaves of the near-sibling subtrees of
 // far steps at depth <= depth(u).  So "min(sibling subtree at far depth l) >
 // max_{far l' >= l} box'(l')" for every far l proves the visit; once visited
-// the unique minimum is never replaced.
+// the unique minimum is never replaced.  A centroid u moved after the
+// snapshot keeps the proof iff its live distance d_u > d(c*) and, when its
+// LCA with c* is a far step, d_u > B[lca]; a moved c* needs d(c*) < m2.
 #include "gsc_tree.h"
 
 namespace gsc {
 
-constexpr int kBatch = 32;  // queries per speculative batch (log window 2*kBatch <= 64)
+constexpr int kBatch = 32;         // queries per speculative batch (log window 2*kBatch <= 64)
+constexpr int kVer = 64 + kBatch;  // centroid versions seen by a pending batch
 
 struct WaveRec {      // A1 output per (wave, query)
     uint32_t minbits; // wave minimum distance (f32 bits; distances are >= 0)
@@ -62,7 +70,7 @@ struct QRec {         // A2 output per query
     float rate;       // Single(1/sqrt(previous-pass count of c*))
     uint32_t farmask; // far steps on c*'s root path, bit = depth
     int pad_;
-    float B[12];      // suffix max of box' over far steps (certificate thresholds)
+    float B[16];      // suffix max of box' over far steps (certificate thresholds)
     float o[16];      // c*'s snapshot coordinates
 };
 
@@ -70,19 +78,31 @@ struct Scan2Shared {
     KdTree t;
     float dist[kMaxK];  // tree build scratch; live distances for the exact DFS
     float rate[kMaxK];  // Single(1/sqrt(cnts[not Odd(iter)])) by kd-leaf position
-    int cnta[kMaxK];    // cnts[Odd(iter)] by kd-leaf position
+    float dfs_inc[kMaxK];  // exact DFS: per split node box' increment, sign = near child hi
     float q[2][kBatch][16];
-    float qslow[16];
-    WaveRec wrec[8][kBatch];
+    float qslow[16];       // the query resolved on its own after a failed commit
+    WaveRec wrec[8][kBatch + 1];  // column kBatch: the solo query
     QRec qrec[2][kBatch];
+    QRec qsolo;
+    // update log: entry e = wave-0 lane e (position in a VGPR, coordinates here)
+    float lg_c[64][16];
     int pub_pos[64];
     float pub_c[64][16];
-    float lg_c[64][16];  // update log coordinates (wave 0's lane t owns entry t)
-    int fail_j, fail_slow;
+    // commit of the pending batch: versions 0..63 = log entries, 64+j = after query j
+    int vpos[kVer];
+    int vfrom[kVer];   // first query that sees the version
+    int vto[kVer];     // last query that sees it
+    float newc[kBatch][16];
+    float gp[kBatch];  // live d(q_j, c*_j)
+    int inval[kBatch];
+    int nxt[kBatch];   // next query of the batch with the same c* (kBatch = none)
+    int ient[kBatch];  // log entry holding c*_j when the commit starts (-1 = none)
+    int freel[64];     // commit: free log entries, in lane order
+    int asg[64];       // commit: log entry -> centroid position it now holds
     int slow_pos;
     float slow_key;
     int any_nan;
-    int st_h[16];       // exact-DFS stack (one lane)
+    int st_h[16];      // exact-DFS stack (one lane)
     float st_box[16];
 };
 
@@ -95,22 +115,18 @@ __device__ __forceinline__ uint64_t stamp() {
     __builtin_amdgcn_sched_barrier(0);
     return t;
 }
-#define STAMP(k)                          \
-    {                                     \
-        const uint64_t t_ = stamp();      \
-        acc[k] += t_ - tlast;             \
-        tlast = t_;                       \
+#define STAMP(k)                     \
+    {                                \
+        const uint64_t t_ = stamp(); \
+        acc[k] += t_ - tlast;        \
+        tlast = t_;                  \
     }
 #else
 #define STAMP(k)
 #endif
 
-__device__ __forceinline__ uint32_t rl(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
-__device__ __forceinline__ float rlf(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
-__device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-
 // value of the lane in the other aligned half of the 2^(b+1) lane group
-// (valid for group-uniform inputs, which the min-tree guarantees)
+// (valid for group-uniform inputs, which the reductions below guarantee)
 template <int B>
 __device__ __forceinline__ uint32_t partner(uint32_t v) {
     if constexpr (B == 0) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
@@ -120,27 +136,64 @@ __device__ __forceinline__ uint32_t partner(uint32_t v) {
     if constexpr (B == 4) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);                      // xor 16
     return 0u;
 }
+__device__ __forceinline__ uint32_t min16(uint32_t v) {  // min over each aligned 16-lane row
+    v = min(v, partner<0>(v));
+    v = min(v, partner<1>(v));
+    v = min(v, partner<2>(v));
+    return min(v, partner<3>(v));
+}
+__device__ __forceinline__ uint32_t sum16(uint32_t v) {
+    v += partner<0>(v);
+    v += partner<1>(v);
+    v += partner<2>(v);
+    return v + partner<3>(v);
+}
+
+// orders this wave's LDS accesses across lanes (lane-to-lane hand-off
+// through LDS inside one wave: without it the compiler may reorder them)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// workgroup barrier that orders LDS only: the loop's global traffic (cluster
+// ids, count atomics, query prefetch) stays in flight across it
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// sequential f32 squared distance (ANN leaf order d = 0..D-1)
+template <int D>
+__device__ __forceinline__ float seqdist(const float* __restrict__ a, const float* __restrict__ b) {
+    float s = 0.0f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const float t = fsub(a[d], b[d]);
+        s = fadd(s, fmul(t, t));
+    }
+    return s;
+}
 
 // ---------------------------------------------------------------------------
 // A1: snapshot distances of one query against this wave's 512 leaves.
 // ---------------------------------------------------------------------------
 template <int D, int LOGK>
-__device__ __forceinline__ void a1_query(Scan2Shared& sh, const float (&creg)[8][D], const float* __restrict__ qv,
-                                         WaveRec& rec, int wave, int lane) {
+__device__ __forceinline__ void a1_query(const float (&creg)[8][D], const float* __restrict__ qv, WaveRec& rec,
+                                         int wave, int lane) {
     constexpr int K = 1 << LOGK;
     const int p0 = (wave * 64 + lane) * 8;
-    float q[D];
-#pragma unroll
-    for (int d = 0; d < D; ++d) q[d] = qv[d];
     // ANN leaf distance (ANN.dll @0x1800128b0): dist = dist + (q[d]-p[d])^2, d = 0..D-1
     float dv[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) dv[s] = 0.0f;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
+        const float qd = qv[d];
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
-            const float t = fsub(q[d], creg[s][d]);
+            const float t = fsub(qd, creg[s][d]);
             dv[s] = fadd(dv[s], fmul(t, t));
         }
     }
@@ -151,19 +204,6 @@ __device__ __forceinline__ void a1_query(Scan2Shared& sh, const float (&creg)[8]
     const uint32_t m01 = min(b[0], b[1]), m23 = min(b[2], b[3]), m45 = min(b[4], b[5]), m67 = min(b[6], b[7]);
     const uint32_t m03 = min(m01, m23), m47 = min(m45, m67);
     const uint32_t lmin = min(m03, m47);
-    int ls = 7, lc = 0;
-#pragma unroll
-    for (int s = 7; s >= 0; --s) {
-        const bool e = b[s] == lmin;
-        lc += e ? 1 : 0;
-        ls = e ? s : ls;
-    }
-    // in-lane sibling minima of slot ls: slot ls^1, pair (ls>>1)^1, quad (ls>>2)^1
-    const uint32_t pa = (ls & 4) ? ((ls & 2) ? b[6] : b[4]) : ((ls & 2) ? b[2] : b[0]);
-    const uint32_t pb = (ls & 4) ? ((ls & 2) ? b[7] : b[5]) : ((ls & 2) ? b[3] : b[1]);
-    const uint32_t s0 = (ls & 1) ? pa : pb;
-    const uint32_t s1 = (ls & 4) ? ((ls & 2) ? m45 : m67) : ((ls & 2) ? m01 : m23);
-    const uint32_t s2 = (ls & 4) ? m03 : m47;
     // wave min-tree: partner group minima are the sibling subtrees on the path
     uint32_t v = lmin;
     const uint32_t sl0 = partner<0>(v);
@@ -176,84 +216,76 @@ __device__ __forceinline__ void a1_query(Scan2Shared& sh, const float (&creg)[8]
     v = min(v, sl3);
     const uint32_t sl4 = partner<4>(v);
     v = min(v, sl4);
-    const uint32_t vlo = rl(v, 0), vhi = rl(v, 32);
-    const uint32_t sl5 = lane < 32 ? vhi : vlo;
+    const uint32_t vlo = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+    const uint32_t vhi = (uint32_t)__builtin_amdgcn_readlane((int)v, 32);
     const uint32_t wmin = min(vlo, vhi);
     const uint64_t m = __ballot(lmin == wmin);
     const int L = __ffsll((long long)m) - 1;
-    const int tie = (__popcll(m) > 1 || (int)rl((uint32_t)lc, L) > 1) ? 1 : 0;
-    const int pos = (wave * 64 + L) * 8 + (int)rl((uint32_t)ls, L);
-    const uint32_t r0 = rl(sl0, L), r1 = rl(sl1, L), r2 = rl(sl2, L), r3 = rl(sl3, L), r4 = rl(sl4, L), r5 = rl(sl5, L);
-    const uint32_t r6 = rl(s0, L), r7 = rl(s1, L), r8 = rl(s2, L);
-    if (lane == 0) {
-        rec.minbits = wmin;
-        rec.tie = tie;
-        rec.pos = pos;
-        rec.sib[0] = r0;
-        rec.sib[1] = r1;
-        rec.sib[2] = r2;
-        rec.sib[3] = r3;
-        rec.sib[4] = r4;
-        rec.sib[5] = r5;
-        rec.sib[6] = r6;
-        rec.sib[7] = r7;
-        rec.sib[8] = r8;
-    }
-}
-
-// global winner of query jj over the NW wave records (first wave at the minimum)
-template <int NW>
-__device__ __forceinline__ void winner(const Scan2Shared& sh, int jj, uint32_t& gmin, int& W, int& nmin) {
-    gmin = 0xFFFFFFFFu;
-    W = 0;
-    nmin = 0;
+    if (lane == L) {
+        int ls = 7, lc = 0;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {
-        const uint32_t m = sh.wrec[w][jj].minbits;
-        if (m < gmin) {
-            gmin = m;
-            W = w;
-            nmin = 1;
-        } else if (m == gmin) {
-            ++nmin;
+        for (int s = 7; s >= 0; --s) {
+            const bool e = b[s] == lmin;
+            lc += e ? 1 : 0;
+            ls = e ? s : ls;
         }
+        // in-lane sibling minima of slot ls: slot ls^1, pair (ls>>1)^1, quad (ls>>2)^1
+        const uint32_t pa = (ls & 4) ? ((ls & 2) ? b[6] : b[4]) : ((ls & 2) ? b[2] : b[0]);
+        const uint32_t pb = (ls & 4) ? ((ls & 2) ? b[7] : b[5]) : ((ls & 2) ? b[3] : b[1]);
+        rec.minbits = wmin;
+        rec.tie = (__popcll(m) > 1 || lc > 1) ? 1 : 0;
+        rec.pos = p0 + ls;
+        rec.sib[0] = sl0;
+        rec.sib[1] = sl1;
+        rec.sib[2] = sl2;
+        rec.sib[3] = sl3;
+        rec.sib[4] = sl4;
+        rec.sib[5] = lane < 32 ? vhi : vlo;
+        rec.sib[6] = (ls & 1) ? pa : pb;
+        rec.sib[7] = (ls & 4) ? ((ls & 2) ? m45 : m67) : ((ls & 2) ? m01 : m23);
+        rec.sib[8] = (ls & 4) ? m03 : m47;
     }
 }
 
 // ---------------------------------------------------------------------------
-// A2: certificate for query jj (one wave, lanes = tree depths).
+// A2: certificates of 4 queries per wave (16 lanes per query, lane = depth).
 // ---------------------------------------------------------------------------
 template <int D, int LOGK, int NW>
-__device__ __forceinline__ void a2_query(Scan2Shared& sh, int jj, int qb, int lane) {
+__device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const float (*qrows)[16], QRec* recs, int wcol0,
+                                         int lane) {
     constexpr int KW = LOGK >= 9 ? LOGK - 9 : 0;  // depths resolved at wave level
-    uint32_t gmin;
-    int W, nmin;
-    winner<NW>(sh, jj, gmin, W, nmin);
-    gmin = rfl(gmin);
-    W = __builtin_amdgcn_readfirstlane(W);
-    nmin = __builtin_amdgcn_readfirstlane(nmin);
-    const WaveRec& r = sh.wrec[W][jj];
-    const int cstar = __builtin_amdgcn_readfirstlane(r.pos);
-    const int tie = (nmin > 1 || r.tie) ? 1 : 0;
-    const float* q = sh.q[qb][jj];
-    // sibling-subtree minimum at depth l, held by lane l
+    const int l = lane & 15, gbase = lane & ~15;
+    const int jj = j0 + (lane >> 4);
+    const bool qa = jj < nq;
+    const int jr = qa ? jj : j0;  // safe index for inactive groups
+    // global winner over the NW wave records (first wave at the minimum)
+    const int wc = wcol0 + jr;
+    const uint32_t mw = (l < NW) ? sh.wrec[l][wc].minbits : 0xFFFFFFFFu;
+    const uint32_t gmin = min16(mw);
+    const uint32_t nmin = sum16((mw == gmin && l < NW) ? 1u : 0u);
+    const int W = (int)min16((mw == gmin && l < NW) ? (uint32_t)l : 99u);
+    const WaveRec& r = sh.wrec[W < NW ? W : 0][wc];
+    const int cstar = r.pos;
+    const bool tie = nmin > 1 || r.tie;
+    const float* q = qrows[jr];
+    // sibling-subtree minimum at depth l
     uint32_t sib = 0xFFFFFFFFu;
-    if (lane < KW) {
-        const int sh_ = KW - 1 - lane;  // sibling wave group of W at depth lane
+    if (l < KW) {
+        const int sh_ = KW - 1 - l;  // sibling wave group of W at depth l
         const int want = (W >> sh_) ^ 1;
 #pragma unroll
         for (int w = 0; w < NW; ++w)
-            if ((w >> sh_) == want) sib = min(sib, sh.wrec[w][jj].minbits);
-    } else if (lane < LOGK) {
-        const int idx = lane <= LOGK - 4 ? (LOGK - 4 - lane) : (lane == LOGK - 3 ? 8 : (lane == LOGK - 2 ? 7 : 6));
+            if ((w >> sh_) == want) sib = min(sib, sh.wrec[w][wc].minbits);
+    } else if (l < LOGK) {
+        const int idx = l <= LOGK - 4 ? (LOGK - 4 - l) : (l == LOGK - 3 ? 8 : (l == LOGK - 2 ? 7 : 6));
         sib = r.sib[idx];
     }
-    // path evaluation: split node at depth l on c*'s root path (ANNkd_split::ann_search)
+    // split node at depth l on c*'s root path (ANNkd_split::ann_search)
     bool far = false;
     float inc = 0.0f;
-    if (lane < LOGK) {
-        const int h = (1 << lane) - 1 + (cstar >> (LOGK - lane));
-        const bool golo = ((cstar >> (LOGK - 1 - lane)) & 1) == 0;
+    if (l < LOGK) {
+        const int h = (1 << l) - 1 + (cstar >> (LOGK - l));
+        const bool golo = ((cstar >> (LOGK - 1 - l)) & 1) == 0;
         const int cdim = sh.t.cd[h];
         const float qc = q[cdim];
         const float cut = fsub(qc, sh.t.cv[h]);
@@ -265,7 +297,7 @@ __device__ __forceinline__ void a2_query(Scan2Shared& sh, int jj, int qb, int la
             inc = fsub(fmul(cut, cut), fmul(bd, bd));
         }
     }
-    const uint64_t farmask = __ballot(far);
+    const uint32_t farmask = (uint32_t)(__ballot(far) >> gbase) & 0xFFFFu;
     // annBoxDistance(q, enclosing rect) in dimension order
     float box = 0.0f;
 #pragma unroll
@@ -279,116 +311,131 @@ __device__ __forceinline__ void a2_query(Scan2Shared& sh, int jj, int qb, int la
             box = fadd(box, fmul(t, t));
         }
     }
-    // box' at far steps, accumulated root -> leaf: box' = (cut^2 - bd^2) + box
-    float boxp = -__builtin_inff();
-    for (int l = 0; l < LOGK; ++l) {
-        if ((farmask >> l) & 1ull) {
-            box = fadd(box, rlf(inc, l));
-            if (lane == l) boxp = box;
+    // box' at far steps, accumulated root -> leaf: box' = (cut^2 - bd^2) + box;
+    // B[l] = max over far steps at depth >= l
+    float incs[LOGK];
+#pragma unroll
+    for (int k = 0; k < LOGK; ++k) incs[k] = __int_as_float(__shfl(__float_as_int(inc), gbase + k));
+    float bp[LOGK];
+#pragma unroll
+    for (int k = 0; k < LOGK; ++k) {
+        bp[k] = -__builtin_inff();
+        if ((farmask >> k) & 1u) {
+            box = fadd(box, incs[k]);
+            bp[k] = box;
         }
     }
     float Bv = -__builtin_inff(), run = -__builtin_inff();
-    for (int l = LOGK - 1; l >= 0; --l) {
-        run = fmaxf(run, rlf(boxp, l));
-        if (lane == l) Bv = run;
+#pragma unroll
+    for (int k = LOGK - 1; k >= 0; --k) {
+        run = fmaxf(run, bp[k]);
+        Bv = (l == k) ? run : Bv;
     }
     const bool ok = !far || (__uint_as_float(sib) > Bv);
-    const bool valid = !tie && __uint_as_float(gmin) <= FLT_MAX && __all(ok);
-    // m2: minimum over all sibling subtrees = every leaf except c*
-    uint32_t m2 = sib;
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) m2 = min(m2, (uint32_t)__shfl_xor((int)m2, o));
-    m2 = rl(m2, 0);
-    QRec& R = sh.qrec[qb][jj];
-    if (lane < LOGK) R.B[lane] = Bv;
-    if (lane == 0) {
-        R.valid = valid ? 1 : 0;
-        R.cstar = cstar;
-        R.id = sh.t.pidx[cstar];
-        R.g = __uint_as_float(gmin);
-        R.m2 = __uint_as_float(m2);
-        R.rate = sh.rate[cstar];
-        R.farmask = (uint32_t)farmask;
+    const bool gok = ((__ballot(!ok) >> gbase) & 0xFFFFull) == 0;
+    const bool valid = !tie && __uint_as_float(gmin) <= FLT_MAX && gok;
+    const uint32_t m2 = min16(sib);  // every leaf except c*
+    if (qa) {
+        QRec& R = recs[jj];
+        if (l < LOGK) R.B[l] = Bv;
+        if (l == 0) {
+            R.valid = valid ? 1 : 0;
+            R.cstar = cstar;
+            R.id = sh.t.pidx[cstar];
+            R.g = __uint_as_float(gmin);
+            R.m2 = __uint_as_float(m2);
+            R.rate = sh.rate[cstar];
+            R.farmask = farmask;
+        }
     }
 }
 
 // ---------------------------------------------------------------------------
-// S: serial commit of a speculated batch (wave 0).  Returns via sh.fail_j.
-// Log: lane t holds entry t = (position lg_pos, live coordinates lg_c,
-// batch tag lg_bt); every centroid moved since the snapshot of the batch
-// being committed is in the log with its live value.
+// Commit, step 1 (wave 0, lanes = queries j of the pending batch): online
+// updates in order per centroid (encoder.lpr:735-740, f32 c += (x - c) * rate)
+// assuming every query of the batch commits; version table for the checks.
+// Log entry e is lane e: position lg_pos (-1 = empty), tag = committing batch.
 // ---------------------------------------------------------------------------
 template <int D, int LOGK>
-__device__ __forceinline__ void s_commit(Scan2Shared& sh, int qb, int ps, int pn, bool pfresh, int pit, int lane,
-                                         int& lg_pos, int& lg_bt, int* __restrict__ clusters,
-                                         double& err) {
-    if (lg_pos >= 0 && lg_bt <= pit - 2) lg_pos = -1;  // already folded into the snapshot
-    int fj = -1, fslow = 0;
-#pragma unroll 1
-    for (int jj = 0; jj < pn; ++jj) {
-        const QRec& R = sh.qrec[qb][jj];
-        const int valid = __builtin_amdgcn_readfirstlane(R.valid);
-        if (!valid) {
-            fj = jj;
-            fslow = (pfresh && jj == 0) ? 1 : 0;
-            break;
-        }
-        const int cstar = __builtin_amdgcn_readfirstlane(R.cstar);
-        const float g = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(R.g)));
-        const float m2 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(R.m2)));
-        const uint32_t farmask = rfl(R.farmask);
-        const float* q = sh.q[qb][jj];
-        float qd[D];
+__device__ __forceinline__ void v_prepare(Scan2Shared& sh, int qb, int off, int pn, int a1, int lane, int& lg_pos,
+                                          int lg_tag) {
+    if (lg_pos >= 0 && lg_tag < a1) lg_pos = -1;  // committed before the batch's snapshot
+    const int j = lane;
+    const bool act = j < pn;
+    const QRec& R = sh.qrec[qb][off + (act ? j : 0)];
+    const int cs = act ? R.cstar : -2;
+    sh.vpos[lane] = lg_pos;
+    sh.vfrom[lane] = 0;
+    wave_lds_sync();
+    int pred = -1, nxt = kBatch, first = kBatch;
+    for (int k = 0; k < pn; ++k) {
+        const int ck = sh.qrec[qb][off + k].cstar;
+        if (k < j && ck == cs) pred = 64 + k;
+        if (k > j && ck == cs && nxt == kBatch) nxt = k;
+        if (ck == lg_pos && first == kBatch) first = k;  // lane as log entry: first query moving it
+    }
+    // log entry holding c*_j (c*_j moved before the batch)
+    int ie = -1;
+    for (int e = 63; e >= 0; --e)
+        if (sh.vpos[e] == cs) ie = e;
+    if (pred < 0) pred = ie;
+    // versions: log entries (0..63) and "after query j" (64+j)
+    sh.vto[lane] = lg_pos >= 0 ? first : -1;
+    if (lane < kBatch) {
+        sh.vpos[64 + lane] = act ? cs : -1;
+        sh.vfrom[64 + lane] = j + 1;
+        sh.vto[64 + lane] = act ? nxt : -1;
+        sh.nxt[lane] = nxt;
+        sh.ient[lane] = ie;
+        sh.inval[lane] = 0;
+    }
+    // chained updates: a query waits for its predecessor's new coordinates
+    uint64_t done = ~__ballot(act);
+    for (;;) {
+        const bool ready = act && !((done >> j) & 1ull) && (pred < 64 || ((done >> (pred - 64)) & 1ull));
+        const uint64_t rm = __ballot(ready);
+        if (!rm) break;
+        if (ready) {
+            const float* qv = sh.q[qb][off + j];
+            const float* o = pred < 0 ? R.o : (pred < 64 ? sh.lg_c[pred] : sh.newc[pred - 64]);
+            float oc[D];
 #pragma unroll
-        for (int d = 0; d < D; ++d) qd[d] = q[d];
-        float du = 0.0f;
-        float* lc = sh.lg_c[lane];
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            const float t = fsub(qd[d], lc[d]);
-            du = fadd(du, fmul(t, t));
-        }
-        const bool act = lg_pos >= 0;
-        const bool isc = act && lg_pos == cstar;
-        const uint64_t mc = __ballot(isc);
-        const int tc = mc ? __ffsll((long long)mc) - 1 : -1;
-        const float gp = tc >= 0 ? rlf(du, tc) : g;
-        const bool okc = tc < 0 || gp < m2;
-        bool oku = true;
-        if (act && !isc) {
-            const int lca = __clz(lg_pos ^ cstar) - (32 - LOGK);
-            const bool farl = (farmask >> lca) & 1u;
-            oku = du > gp && (!farl || du > R.B[lca]);
-        }
-        if (!(okc && __all(oku))) {
-            fj = jj;
-            fslow = (pfresh && jj == 0) ? 1 : 0;
-            break;
-        }
-        // online update of c* (encoder.lpr:735-740), f32: c += (x - c) * rate
-        const float rate = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(R.rate)));
-        const int e = tc >= 0 ? tc : __ffsll((long long)__ballot(lg_pos < 0)) - 1;
-        if (lane == e) {
-#pragma unroll
-            for (int d = 0; d < D; ++d) {
-                const float o = tc >= 0 ? lc[d] : R.o[d];
-                lc[d] = fadd(o, fmul(fsub(qd[d], o), rate));
+            for (int d = 0; d < D; ++d) oc[d] = o[d];
+            float gpj = R.g;
+            bool okc = R.valid != 0;
+            if (pred >= 0) {
+                gpj = seqdist<D>(qv, oc);
+                okc = okc && gpj < R.m2;
             }
-            lg_pos = cstar;
-            lg_bt = pit;
+            const float rate = R.rate;
+#pragma unroll
+            for (int d = 0; d < D; ++d) sh.newc[j][d] = fadd(oc[d], fmul(fsub(qv[d], oc[d]), rate));
+            sh.gp[j] = gpj;
+            if (!okc) sh.inval[j] = 1;
         }
-        if (lane == 0) {
-            sh.cnta[cstar] += 1;
-            clusters[ps + jj] = R.id;
-            err += (double)__fsqrt_rn(gp / (float)D);  // encoder.lpr:743
-        }
+        wave_lds_sync();  // this round's newc feed the next round's lanes
+        done |= rm;
     }
-    if (fslow) {
-        if (lane < D) sh.qslow[lane] = sh.q[qb][fj][lane];
-    }
-    if (lane == 0) {
-        sh.fail_j = fj;
-        sh.fail_slow = fslow;
+}
+
+// Commit, step 2 (all threads): every (query, moved centroid) pair of the
+// pending batch -- the moved centroid must stay provably outside ANN's answer.
+template <int D, int LOGK>
+__device__ __forceinline__ void v_check(Scan2Shared& sh, int qb, int off, int pn, int tid, int nthreads) {
+    const int npairs = pn * kVer;
+    for (int p = tid; p < npairs; p += nthreads) {
+        const int j = p / kVer, v = p - j * kVer;
+        const int vp = sh.vpos[v];
+        if (vp < 0 || j < sh.vfrom[v] || j > sh.vto[v]) continue;
+        const QRec& R = sh.qrec[qb][off + j];
+        const int cs = R.cstar;
+        if (vp == cs) continue;  // c* itself: checked in v_prepare
+        const float* c = v < 64 ? sh.lg_c[v] : sh.newc[v - 64];
+        const float du = seqdist<D>(sh.q[qb][off + j], c);
+        const float g = sh.gp[j];
+        const int lca = __clz(vp ^ cs) - (32 - LOGK);
+        const bool farl = (R.farmask >> lca) & 1u;
+        if (!(du > g && (!farl || du > R.B[lca]))) sh.inval[j] = 1;
     }
 }
 
@@ -396,68 +443,77 @@ __device__ __forceinline__ void s_commit(Scan2Shared& sh, int qb, int ps, int pn
 // stale tree with the live leaf distances in sh.dist -- one lane, stack in
 // LDS.  No NaN distances reach this kernel (those passes run the generic
 // kernel), so leaf early exits cannot change a result.
+// Exact ANN ann_search (k = 1, eps = 0; annkSearch @0x1800124b0) over the
+// stale tree with the live leaf distances in sh.dist, for the query in
+// sh.qslow.  All threads first tabulate every split node's near child and
+// box' increment (ANNkd_split::ann_search: cut = q[cd] - cv; bd = lo - q[cd]
+// or q[cd] - hi, clamped at 0; box' = (cut^2 - bd^2) + box), then one lane
+// walks the DFS with the stack in LDS.  No NaN distances reach this kernel
+// (those passes run the generic kernel), so leaf early exits cannot change a
+// result.
 template <int D, int LOGK>
-__device__ __forceinline__ void dfs_exact(Scan2Shared& sh, int& out_pos, float& out_key) {
+__device__ __forceinline__ void dfs_exact(Scan2Shared& sh, int tid, int nthreads) {
     constexpr int K = 1 << LOGK;
     const float* q = sh.qslow;
-    float cur_box = 0.0f;
-    for (int d = 0; d < D; ++d) {  // annBoxDistance
-        const float qd = q[d];
-        if (sh.t.bnd_lo[d] > qd) {
-            const float t = fsub(sh.t.bnd_lo[d], qd);
-            cur_box = fadd(cur_box, fmul(t, t));
-        } else if (qd > sh.t.bnd_hi[d]) {
-            const float t = fsub(qd, sh.t.bnd_hi[d]);
-            cur_box = fadd(cur_box, fmul(t, t));
-        }
-    }
-    int h = 0, sp = 0, best = -1;
-    float key = FLT_MAX;
-    for (;;) {
-        if (h >= K - 1) {
-            // ANNkd_leaf::ann_search: insert iff the list is empty or key > dist
-            const int p = h - (K - 1);
-            const float dd = sh.dist[p];
-            if (best < 0 || key > dd) {
-                key = dd;
-                best = p;
-            }
-            // unwind: the far child is visited iff box' < max_key
-            bool found = false;
-            while (sp > 0) {
-                --sp;
-                if (sh.st_box[sp] < key) {
-                    h = sh.st_h[sp];
-                    cur_box = sh.st_box[sp];
-                    found = true;
-                    break;
-                }
-            }
-            if (!found) break;
-            continue;
-        }
+    for (int h = tid; h < K - 1; h += nthreads) {
         const int cdim = sh.t.cd[h];
         const float qc = q[cdim];
         const float cut = fsub(qc, sh.t.cv[h]);
-        float bd;
-        int nearh, farh;
-        if (cut < 0.0f) {
-            bd = fsub(sh.t.lo[h], qc);
-            nearh = 2 * h + 1;
-            farh = 2 * h + 2;
-        } else {
-            bd = fsub(qc, sh.t.hi[h]);
-            nearh = 2 * h + 2;
-            farh = 2 * h + 1;
-        }
+        const bool nearlo = cut < 0.0f;
+        float bd = nearlo ? fsub(sh.t.lo[h], qc) : fsub(qc, sh.t.hi[h]);
         if (bd < 0.0f) bd = 0.0f;
-        sh.st_box[sp] = fadd(cur_box, fsub(fmul(cut, cut), fmul(bd, bd)));
-        sh.st_h[sp] = farh;
-        ++sp;
-        h = nearh;
+        const float inc = fsub(fmul(cut, cut), fmul(bd, bd));  // >= +0
+        sh.dfs_inc[h] = nearlo ? inc : -inc;
     }
-    out_pos = best;
-    out_key = key;
+    lds_barrier();
+    if (tid == 0) {
+        float cur_box = 0.0f;
+        for (int d = 0; d < D; ++d) {  // annBoxDistance
+            const float qd = q[d];
+            if (sh.t.bnd_lo[d] > qd) {
+                const float t = fsub(sh.t.bnd_lo[d], qd);
+                cur_box = fadd(cur_box, fmul(t, t));
+            } else if (qd > sh.t.bnd_hi[d]) {
+                const float t = fsub(qd, sh.t.bnd_hi[d]);
+                cur_box = fadd(cur_box, fmul(t, t));
+            }
+        }
+        int h = 0, sp = 0, best = -1;
+        float key = FLT_MAX;
+        for (;;) {
+            if (h >= K - 1) {
+                // ANNkd_leaf::ann_search: insert iff the list is empty or key > dist
+                const int p = h - (K - 1);
+                const float dd = sh.dist[p];
+                if (best < 0 || key > dd) {
+                    key = dd;
+                    best = p;
+                }
+                // unwind: the far child is visited iff box' < max_key
+                bool found = false;
+                while (sp > 0) {
+                    --sp;
+                    if (sh.st_box[sp] < key) {
+                        h = sh.st_h[sp];
+                        cur_box = sh.st_box[sp];
+                        found = true;
+                        break;
+                    }
+                }
+                if (!found) break;
+                continue;
+            }
+            const float v = sh.dfs_inc[h];
+            const int hi = __float_as_uint(v) >> 31;
+            sh.st_box[sp] = fadd(cur_box, fabsf(v));
+            sh.st_h[sp] = 2 * h + 2 - hi;
+            ++sp;
+            h = 2 * h + 1 + hi;
+        }
+        sh.slow_pos = best;
+        sh.slow_key = key;
+    }
+    lds_barrier();
 }
 
 // fold published log entries into the owners' registers
@@ -500,11 +556,13 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
     const float* __restrict__ X = uniform_ptr(Xall + frp->x_off);
     float* C = uniform_ptr(Call + frp->c_off);
     int* clusters = uniform_ptr(i_scratch + frp->n_off);
-    int* prev_cnt = uniform_ptr(i_scratch + frp->k_off);
+    int* prev_cnt = uniform_ptr(i_scratch + frp->k_off);  // cnts[not Odd(iter)] by centroid id
+    int* cnta = uniform_ptr(i_scratch + frp->ka_off);     // cnts[Odd(iter)] by kd-leaf position
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nthreads = 64 * NW;
 
     if (pass == 0)
-        for (int k = tid; k < K; k += blockDim.x) prev_cnt[k] = 1;  // CCntStart (encoder.lpr:717-721)
+        for (int k = tid; k < K; k += nthreads) prev_cnt[k] = 1;  // CCntStart (encoder.lpr:717-721)
     if (tid == 0) sh.any_nan = 0;
     __syncthreads();
     build_tree<D>(sh.t, sh.dist, C, K);
@@ -523,7 +581,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
                 nan_here |= creg[s][d] != creg[s][d];
             }
             sh.rate[p] = rate_tab[prev_cnt[id]];
-            sh.cnta[p] = 1;
+            cnta[p] = 1;
         } else {
 #pragma unroll
             for (int d = 0; d < D; ++d) creg[s][d] = 0.0f;
@@ -532,7 +590,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
     if (nan_here) sh.any_nan = 1;
     // first batch's queries
     const int n0 = min(kBatch, N);
-    for (int k = tid; k < n0 * D; k += blockDim.x) sh.q[0][k / D][k % D] = X[k];
+    for (int k = tid; k < n0 * D; k += nthreads) sh.q[0][k / D][k % D] = X[k];
     __syncthreads();
     if (uniform_int(sh.any_nan)) {
         // NaN centroids (yakmo 0/0 means) make ANN's early exits order dependent:
@@ -541,162 +599,250 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
         return;
     }
 
-    // wave-0 state: update log + residual
-    int lg_pos = -1, lg_bt = 0;
+    // wave-0 state: update log (lane = entry, tag = commit iteration) + residual (lane 0)
+    int lg_pos = -1, lg_tag = 0;
     double err = 0.0;
     int slow_total = 0, restarts = 0;
-
 #ifdef GSC_STAMPS
     uint64_t acc[6] = {0, 0, 0, 0, 0, 0};
     uint64_t tlast = stamp();
 #endif
-    int cur_s = 0, cur_n = n0, cbuf = 0;
-    bool cur_fresh = true;
-    int pend_s = 0, pend_n = 0, pbuf = 1, pit = 0;
-    bool pend_fresh = false;
+    // batches awaiting commit, in order: buffer, first query of the buffer,
+    // first uncommitted slot, count, iteration of their distance snapshot
+    int vq_buf[2] = {0, 0}, vq_s[2] = {0, 0}, vq_off[2] = {0, 0}, vq_n[2] = {0, 0}, vq_a1[2] = {0, 0};
+    int nvq = 0;
+    int cur_buf = 0, cur_s = 0, cur_n = n0;  // batch whose distances are computed this iteration
+    int next_load = n0;
     for (int it = 0;; ++it) {
-        // ---- part 1: S(pending) on wave 0, A1(current) on every wave
-        if (wave == 0) {
-            if (pend_n > 0)
-                s_commit<D, LOGK>(sh, pbuf, pend_s, pend_n, pend_fresh, pit, lane, lg_pos, lg_bt, clusters, err);
-            else if (lane == 0) {
-                sh.fail_j = -1;
-                sh.fail_slow = 0;
-            }
+        const bool has_p = nvq > 0;
+        const int P_buf = vq_buf[0], P_s = vq_s[0], P_off = vq_off[0], P_n = has_p ? vq_n[0] : 0;
+        // prefetch the next batch's queries (they land in LDS in part 3)
+        constexpr int PE = (kBatch * D + 64 * NW - 1) / (64 * NW);
+        float pre[PE];
+#pragma unroll
+        for (int e = 0; e < PE; ++e) {
+            const int k = tid + e * nthreads;
+            pre[e] = (k < kBatch * D && next_load + k / D < N) ? X[(int64_t)next_load * D + k] : 0.0f;
         }
+        // ---- part 1: chain the pending batch's updates (wave 0); A1(current)
+        if (wave == 0 && has_p) v_prepare<D, LOGK>(sh, P_buf, P_off, P_n, vq_a1[0], lane, lg_pos, lg_tag);
         STAMP(0)
 #pragma unroll 1
-        for (int jj = 0; jj < cur_n; ++jj) a1_query<D, LOGK>(sh, creg, sh.q[cbuf][jj], sh.wrec[wave][jj], wave, lane);
+        for (int jj = 0; jj < cur_n; ++jj) a1_query<D, LOGK>(creg, sh.q[cur_buf][jj], sh.wrec[wave][jj], wave, lane);
         STAMP(1)
-        __syncthreads();
-        STAMP(2)
-        // ---- part 2
-        const int fj = uniform_int(sh.fail_j), fslow = uniform_int(sh.fail_slow);
-        int next_s;
-        bool next_fresh;
-        if (fj >= 0) {
-            next_s = pend_s + fj + (fslow ? 1 : 0);
-            next_fresh = true;
-            ++restarts;
-        } else {
-            next_s = cur_s + cur_n;
-            next_fresh = false;
-            if (cur_n > 0) {
-                // c*'s snapshot coordinates, written by the wave that owns c*
-                uint64_t won = 0;
-                {
-                    uint32_t gm;
-                    int W = 0, nm;
-                    if (lane < cur_n) winner<NW>(sh, lane, gm, W, nm);
-                    won = __ballot(lane < cur_n && W == wave);
-                }
-                while (won) {
-                    const int jj = __ffsll((long long)won) - 1;
-                    won &= won - 1;
-                    const int p = sh.wrec[wave][jj].pos;
-                    const int owner = (p >> 3) & 63, slot = p & 7;
+        lds_barrier();
+        // ---- part 2: check the pending batch; certificates of the current batch
+        if (has_p) v_check<D, LOGK>(sh, P_buf, P_off, P_n, tid, nthreads);
+        if (cur_n > 0) {
+            // c*'s snapshot coordinates, written by the wave that owns c*
+            uint64_t won;
+            {
+                const int jq = lane < cur_n ? lane : 0;
+                uint32_t gm = 0xFFFFFFFFu;
+                int W = 0;
 #pragma unroll
-                    for (int s = 0; s < 8; ++s)
-                        if (s == slot && lane == owner) {
-#pragma unroll
-                            for (int d = 0; d < D; ++d) sh.qrec[cbuf][jj].o[d] = creg[s][d];
-                        }
+                for (int w = 0; w < NW; ++w) {
+                    const uint32_t m = sh.wrec[w][jq].minbits;
+                    if (m < gm) {
+                        gm = m;
+                        W = w;
+                    }
                 }
+                won = __ballot(lane < cur_n && W == wave);
+            }
+            while (won) {
+                const int jj = __ffsll((long long)won) - 1;
+                won &= won - 1;
+                const int p = sh.wrec[wave][jj].pos;
+                const int owner = (p >> 3) & 63, slot = p & 7;
+#pragma unroll
+                for (int s = 0; s < 8; ++s)
+                    if (s == slot && lane == owner) {
+#pragma unroll
+                        for (int d = 0; d < D; ++d) sh.qrec[cur_buf][jj].o[d] = creg[s][d];
+                    }
+            }
 #pragma unroll 1
-                for (int jj = wave; jj < cur_n; jj += NW) a2_query<D, LOGK, NW>(sh, jj, cbuf, lane);
+            for (int j0 = wave * 4; j0 < cur_n; j0 += 4 * NW)
+                a2_group<D, LOGK, NW>(sh, j0, cur_n, sh.q[cur_buf], sh.qrec[cur_buf], 0, lane);
+        }
+        STAMP(2)
+        lds_barrier();
+        STAMP(3)
+        // ---- part 3: commit the valid prefix of the pending batch
+        int fj = -1;
+        if (has_p) {
+            const uint64_t bad = __ballot(lane < P_n && sh.inval[lane] != 0);
+            fj = bad ? __ffsll((long long)bad) - 1 : -1;
+        }
+        if (wave == 0 && has_p) {
+            const int k = fj >= 0 ? fj : P_n;
+            const int j = lane;
+            const bool cj = j < k;
+            const QRec& R = sh.qrec[P_buf][P_off + (cj ? j : 0)];
+            if (cj) {
+                clusters[P_s + P_off + j] = R.id;
+                atomicAdd(&cnta[R.cstar], 1);
+            }
+            // residual, in query order (encoder.lpr:743): err += sqrt(best / colCount)
+            const float sq = cj ? __fsqrt_rn(sh.gp[j] / (float)D) : 0.0f;
+            for (int jj = 0; jj < k; ++jj) err += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(sq), jj));
+            // the last committed update of each centroid becomes its log entry:
+            // the entry already holding that centroid, else the r-th free entry
+            const bool lastc = cj && sh.nxt[j] >= k;
+            int tgt = lastc ? sh.ient[j] : -1;
+            const uint64_t need = __ballot(lastc && tgt < 0);
+            const uint64_t freem = __ballot(lg_pos < 0);
+            const uint64_t below = (1ull << lane) - 1ull;
+            sh.asg[lane] = -1;
+            if (lg_pos < 0) sh.freel[__popcll(freem & below)] = lane;
+            wave_lds_sync();
+            if (lastc && tgt < 0) tgt = sh.freel[__popcll(need & below)];
+            if (lastc) {
+#pragma unroll
+                for (int d = 0; d < D; ++d) sh.lg_c[tgt][d] = sh.newc[j][d];
+                sh.asg[tgt] = R.cstar;
+            }
+            wave_lds_sync();
+            const int a = sh.asg[lane];
+            if (a >= 0) {
+                lg_pos = a;
+                lg_tag = it;
+            }
+            if (fj >= 0 && lane < D) sh.qslow[lane] = sh.q[P_buf][P_off + fj][lane];
+        }
+        // queue bookkeeping (uniform)
+        const int solo_j = fj >= 0 ? P_s + P_off + fj : -1;
+        if (has_p) {
+            if (fj >= 0 && fj + 1 < P_n) {
+                vq_off[0] = P_off + fj + 1;
+                vq_n[0] = P_n - fj - 1;
+            } else {
+                vq_buf[0] = vq_buf[1];
+                vq_s[0] = vq_s[1];
+                vq_off[0] = vq_off[1];
+                vq_n[0] = vq_n[1];
+                vq_a1[0] = vq_a1[1];
+                --nvq;
             }
         }
-        STAMP(3)
-        const int nbuf = cbuf ^ 1;  // the pending batch's buffer (S is done with it)
-        const int next_n = max(0, min(kBatch, N - next_s));
-        for (int k = tid; k < next_n * D; k += blockDim.x)
-            sh.q[nbuf][k / D][k % D] = X[(int64_t)next_s * D + k];
-        if (wave == 0) {
-            sh.pub_pos[lane] = lg_pos;
-            if (lg_pos >= 0) {
+        if (cur_n > 0) {
+            vq_buf[nvq] = cur_buf;
+            vq_s[nvq] = cur_s;
+            vq_off[nvq] = 0;
+            vq_n[nvq] = cur_n;
+            vq_a1[nvq] = it;
+            ++nvq;
+        }
+        // next batch of distances: into a free buffer, never the buffer a
+        // failed query's coordinates are being copied out of (wave 0, above)
+        cur_n = 0;
+        const int freeb = nvq == 0 ? (fj >= 0 ? P_buf ^ 1 : 0) : (nvq == 1 ? vq_buf[0] ^ 1 : -1);
+        if (freeb >= 0 && !(fj >= 0 && freeb == P_buf) && next_load < N) {
+            cur_buf = freeb;
+            cur_s = next_load;
+            cur_n = min(kBatch, N - next_load);
+            next_load += cur_n;
+#pragma unroll
+            for (int e = 0; e < PE; ++e) {
+                const int k = tid + e * nthreads;
+                if (k < cur_n * D) sh.q[cur_buf][k / D][k % D] = pre[e];
+            }
+        }
+        if (wave == 0) {  // publish this iteration's commits (earlier ones are in the registers)
+            const bool fresh_e = lg_pos >= 0 && lg_tag == it;
+            sh.pub_pos[lane] = fresh_e ? lg_pos : -1;
+            if (fresh_e) {
 #pragma unroll
                 for (int d = 0; d < D; ++d) sh.pub_c[lane][d] = sh.lg_c[lane][d];
             }
         }
-        __syncthreads();
+        lds_barrier();
         STAMP(4)
-        // ---- part 3: fold the log into the registers
+        // ---- part 4: fold the log into the registers
         refresh<D>(sh, creg, wave, lane);
-        if (fj >= 0 && wave == 0) lg_pos = -1;  // everything is in the registers now
-        if (fslow) {
-            // genuine certificate failure on a fresh snapshot: exact ANN DFS
-            const int j = pend_s + fj;
-            float dv[8];
+        if (solo_j >= 0) {
+            // the failed query on the live centroids: fresh distances and
+            // certificate; exact DFS if the certificate still fails
+            ++restarts;
+            a1_query<D, LOGK>(creg, sh.qslow, sh.wrec[wave][kBatch], wave, lane);
+            lds_barrier();
+            if (wave == 0)
+                a2_group<D, LOGK, NW>(sh, 0, 1, reinterpret_cast<const float(*)[16]>(sh.qslow), &sh.qsolo, kBatch,
+                                      lane);
+            lds_barrier();
+            int bpos;
+            float key;
+            if (uniform_int(sh.qsolo.valid)) {
+                bpos = uniform_int(sh.qsolo.cstar);
+                key = sh.qsolo.g;
+            } else {
+                float dv[8];
 #pragma unroll
-            for (int s = 0; s < 8; ++s) dv[s] = 0.0f;
+                for (int s = 0; s < 8; ++s) dv[s] = 0.0f;
 #pragma unroll
-            for (int d = 0; d < D; ++d) {
-                const float qd = sh.qslow[d];
+                for (int d = 0; d < D; ++d) {
+                    const float qd = sh.qslow[d];
 #pragma unroll
-                for (int s = 0; s < 8; ++s) {
-                    const float t = fsub(qd, creg[s][d]);
-                    dv[s] = fadd(dv[s], fmul(t, t));
+                    for (int s = 0; s < 8; ++s) {
+                        const float t = fsub(qd, creg[s][d]);
+                        dv[s] = fadd(dv[s], fmul(t, t));
+                    }
                 }
-            }
-#pragma unroll
-            for (int s = 0; s < 8; ++s)
-                if (p0 + s < K) sh.dist[p0 + s] = dv[s];
-            __syncthreads();
-            if (tid == 0) dfs_exact<D, LOGK>(sh, sh.slow_pos, sh.slow_key);
-            __syncthreads();
-            const int bpos = uniform_int(sh.slow_pos);
-            if (bpos >= 0) {
-                // owner publishes c's coordinates; tid 0 moves it (encoder.lpr:735-744)
-                // and the move is folded in through the refresh path
-                const int owner = bpos >> 3, slot = bpos & 7;
 #pragma unroll
                 for (int s = 0; s < 8; ++s)
-                    if (s == slot && tid == owner) {
+                    if (p0 + s < K) sh.dist[p0 + s] = dv[s];
+                dfs_exact<D, LOGK>(sh, tid, nthreads);
+                bpos = uniform_int(sh.slow_pos);
+                key = sh.slow_key;
+                ++slow_total;
+            }
+            // owner publishes c's coordinates; tid 0 moves it (encoder.lpr:735-744);
+            // the move enters the log (later batches' snapshots miss it) and the registers
+            const int owner = bpos >> 3, slot = bpos & 7;
 #pragma unroll
-                        for (int d = 0; d < D; ++d) sh.pub_c[0][d] = creg[s][d];
-                    }
-                if (tid < 64) sh.pub_pos[tid] = tid == 0 ? bpos : -1;
-                __syncthreads();
-                if (tid == 0) {
-                    const float key = sh.slow_key;
+            for (int s = 0; s < 8; ++s)
+                if (s == slot && tid == owner) {
+#pragma unroll
+                    for (int d = 0; d < D; ++d) sh.pub_c[0][d] = creg[s][d];
+                }
+            lds_barrier();
+            if (wave == 0) {
+                if (lane == 0) {
                     const float rate = sh.rate[bpos];
                     for (int d = 0; d < D; ++d) {
                         const float o = sh.pub_c[0][d];
                         sh.pub_c[0][d] = fadd(o, fmul(fsub(sh.qslow[d], o), rate));
                     }
-                    sh.cnta[bpos] += 1;
-                    clusters[j] = sh.t.pidx[bpos];
+                    atomicAdd(&cnta[bpos], 1);
+                    clusters[solo_j] = sh.t.pidx[bpos];
                     err += (double)__fsqrt_rn(key / (float)D);
                 }
-                __syncthreads();
-                refresh<D>(sh, creg, wave, lane);
+                wave_lds_sync();
+                const uint64_t hit = __ballot(lg_pos == bpos);
+                const int e = hit ? __ffsll((long long)hit) - 1 : __ffsll((long long)__ballot(lg_pos < 0)) - 1;
+                if (lane == e) {
+                    lg_pos = bpos;
+                    lg_tag = it;
+#pragma unroll
+                    for (int d = 0; d < D; ++d) sh.lg_c[e][d] = sh.pub_c[0][d];
+                }
+                sh.pub_pos[lane] = lane == 0 ? bpos : -1;
             }
-            ++slow_total;
-            __syncthreads();
+            lds_barrier();
+            refresh<D>(sh, creg, wave, lane);
         }
         STAMP(5)
-        if (fj >= 0) {
-            pend_n = 0;
-        } else {
-            pend_s = cur_s;
-            pend_n = cur_n;
-            pbuf = cbuf;
-            pend_fresh = cur_fresh;
-            pit = it;
-        }
-        cur_s = next_s;
-        cur_n = next_n;
-        cbuf = nbuf;
-        cur_fresh = next_fresh;
-        if (cur_n == 0 && pend_n == 0) {
+        if (nvq == 0 && cur_n == 0) {
             if (tid == 0) frp->loop_iters = it + 1;
             break;
         }
-        if (it > 4 * N + 64) {  // progress guard: every query commits within 3 iterations
+        if (it > 4 * N + 64) {  // progress guard: every iteration commits or computes
             if (tid == 0) frp->loop_iters = -1;
             break;
         }
     }
+    __syncthreads();
     // write back the live centroids and this pass's counts (cnts[Odd(iter)])
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
@@ -705,7 +851,8 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
             const int id = sh.t.pidx[p];
 #pragma unroll
             for (int d = 0; d < D; ++d) C[(int64_t)id * D + d] = creg[s][d];
-            prev_cnt[id] = sh.cnta[p];
+            // the commits' atomics live in L2: read past this CU's L1
+            prev_cnt[id] = __hip_atomic_load(&cnta[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 #ifdef GSC_STAMPS
