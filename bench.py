@@ -59,9 +59,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--seconds", type=float, default=64.0, help="audio seconds per GPU")
+    ap.add_argument("--seconds", type=float, default=1024.0,
+                    help="audio seconds per GPU (1024 s = 256 frames of 4 s: one frame per CU)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--cpu-seconds", type=float, default=1.5, help="oracle baseline sample length")
+    ap.add_argument("--cpu-seconds", type=float, default=1.0, help="oracle baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 

@@ -94,7 +94,7 @@ void yakmo_load_train_data(yakmo_t* ay, unsigned int rowCount, unsigned int colC
 
 void yakmo_train_on_data(yakmo_t* ay, int* pointToCluster) {
     const int N = int(ay->rows), D = int(ay->cols), K = int(ay->k);
-    if (!ay->supported || K <= 0 || K >= N || !(D == 8 || D == 16 || D == 32)) {
+    if (!ay->supported || K <= 0 || K >= N || N > 262144 || !(D == 8 || D == 16 || D == 32)) {
         abi_error("yakmo_train_on_data", "unsupported configuration");
         return;
     }
@@ -102,7 +102,7 @@ void yakmo_train_on_data(yakmo_t* ay, int* pointToCluster) {
     fr.N = N;
     fr.K = K;
     fr.k_off = N;
-    float *dX = dalloc<float>(ay->data.size()), *dC = dalloc<float>(size_t(K) * D), *dF = dalloc<float>(3 * size_t(N));
+    float *dX = dalloc<float>(ay->data.size()), *dC = dalloc<float>(size_t(K) * D), *dF = dalloc<float>(4 * size_t(N));
     int* dI = dalloc<int>(size_t(N) + K);
     uint32_t* dB = dalloc<uint32_t>(size_t(N) / 32 + 4);
     gsc::ReduceFrame* dFr = dalloc<gsc::ReduceFrame>(1);

@@ -1,9 +1,10 @@
 // SoundChunks encode hot path on MI355X (gfx950): hand-written HIP kernels.
 //
-//   yakmo_seed_kernel   yakmo_single.dll k-means++ seeding + seeding means
-//                       (encoder.lpr:824-828)   one wave / frame
-//   scan_reduce_kernel  TFrame.KNNScanReduce over ANN's stale kd-tree
-//                       (encoder.lpr:699-765; ANN.dll App. C.2)      one CU / frame
+//   scan_pass_kernel    TFrame.KNNScanReduce over ANN's stale kd-tree, one
+//                       search at a time (encoder.lpr:699-765; ANN.dll App.
+//                       C.2), one CU / frame: the generic path for shapes and
+//                       passes the batched kernel (gsc_scan.hip) does not take
+//   (yakmo seeding: gsc_yakmo.hip)
 //   knnfit_kernel       TFrame.KNNFit 64-NN + tie rule (encoder.lpr:915-965)
 //
 // Everything is bit-exact with the reference's SSE scalar arithmetic: no FMA
@@ -19,141 +20,6 @@
 
 namespace gsc {
 
-
-// ============================================================================
-// yakmo k-means++ seeding (yakmo_single.dll @0x1800016f0) + centroid means
-// (@0x180002290).  One wave per frame.  Per pick: one pass over all points
-// (lanes = points), then the reference's sequential f32 prefix sum cum[]
-// (lane 0 walks the 64 values of each chunk through LDS).
-// ============================================================================
-template <int D>
-__global__ __launch_bounds__(64) void yakmo_seed_kernel(const ReduceFrame* __restrict__ frames, int nframes,
-                                                         const float* __restrict__ Xall, float* __restrict__ Call,
-                                                         float* __restrict__ f_scratch, int* __restrict__ i_scratch,
-                                                         uint32_t* __restrict__ bits_scratch) {
-    const int fi = blockIdx.x;
-    if (fi >= nframes) return;
-    const ReduceFrame fr = frames[fi];
-    const int N = fr.N, K = fr.K;
-    const float* X = Xall + fr.x_off;
-    float* C = Call + fr.c_off;
-    // scratch: per point d0, cum, norm (floats) and id (int) at n_off*4 ...
-    float* d0 = f_scratch + fr.n_off * 3;
-    float* cum = d0 + N;
-    float* norm = cum + N;
-    int* idv = i_scratch + fr.n_off;
-    uint32_t* chosen = bits_scratch + (fr.n_off >> 5) + fi;  // N/32+1 words per frame
-    float* sums = Call + fr.c_off;                            // accumulate into C, divide at the end
-    int* counts = i_scratch + fr.k_off + 0;                   // K ints (k_off region of i_scratch)
-
-    __shared__ float s_d0[64];
-    __shared__ float s_cum[64];
-    const int lane = threadIdx.x;
-
-    // yakmo point norm: norm += v*v (f32, in order) (@0x1800015cb)
-    for (int n = lane; n < N; n += 64) {
-        const float* x = X + (int64_t)n * D;
-        float s = 0.0f;
-#pragma unroll
-        for (int j = 0; j < D; ++j) s = fadd(s, fmul(x[j], x[j]));
-        norm[n] = s;
-    }
-    for (int w = lane; w <= (N >> 5); w += 64) chosen[w] = 0u;
-    __syncthreads();
-
-    uint64_t rx = 123456789ull, ry = 362436069ull, rz = 521288629ull, rw = 88675123ull;
-    float total = 0.0f;
-    for (int i = 0; i < K; ++i) {
-        const uint64_t t = rx ^ (rx << 11);
-        rx = ry;
-        ry = rz;
-        rz = rw;
-        rw = rw ^ (rw >> 19) ^ t ^ (t >> 8);
-        const float r = (float)((double)rw * 5.42101086242752217e-20);
-        uint32_t idx;
-        if (i == 0) {
-            idx = (uint32_t)(int64_t)floorf(fmul(r, (float)N));
-        } else {
-            const float target = fmul(r, total);
-            int64_t first = 0, count = N;
-            while (count > 0) {
-                const int64_t half = count >> 1;
-                const int64_t mid = first + half;
-                const float cm = ld_relaxed(cum + mid);
-                if (target > cm) {
-                    first = mid + 1;
-                    count -= half + 1;
-                } else {
-                    count = half;
-                }
-            }
-            idx = (uint32_t)(int64_t)(float)first;
-        }
-        // collision walk (@0x180001b20) and clamp (@0x180001c50)
-        while (idx < (uint32_t)N && ((ld_relaxed(chosen + (idx >> 5)) >> (idx & 31)) & 1u))
-            idx = (idx < (uint32_t)(N - 1)) ? idx + 1 : 0u;
-        if (idx >= (uint32_t)N) idx = (uint32_t)(N - 1);
-        if (lane == 0) chosen[idx >> 5] |= 1u << (idx & 31);
-        float c[D];
-        const float* xc = X + (int64_t)idx * D;
-#pragma unroll
-        for (int j = 0; j < D; ++j) c[j] = xc[j];
-        const float cn = ld_relaxed(norm + idx);
-
-        float run = 0.0f;  // lane 0 carries the running total
-        const bool last = (i == K - 1);
-        for (int base = 0; base < N; base += 64) {
-            const int n = base + lane;
-            float dn = 0.0f;
-            if (n < N) {
-                const float* x = X + (int64_t)n * D;
-                float d = fadd(fadd(cn, norm[n]), 0.0f);
-#pragma unroll
-                for (int j = 0; j < D; ++j) d = fsub(d, fmul(fadd(x[j], x[j]), c[j]));
-                dn = (i == 0) ? d : d0[n];
-                if (i == 0 || dn > d) {
-                    dn = d;
-                    d0[n] = d;
-                    idv[n] = i;
-                }
-            }
-            if (!last) {
-                s_d0[lane] = dn;
-                __syncthreads();
-                if (lane == 0) {
-                    const int cnt = min(64, N - base);
-                    for (int l = 0; l < cnt; ++l) {
-                        run = fadd(run, s_d0[l]);
-                        s_cum[l] = run;
-                    }
-                }
-                __syncthreads();
-                if (n < N) cum[n] = s_cum[lane];
-                __syncthreads();
-            }
-        }
-        total = __shfl(run, 0);
-        __syncthreads();
-    }
-    // centroid means of the seeding assignment: sum in point order (@0x180001ee0)
-    for (int k = lane; k < K * D; k += 64) sums[k] = 0.0f;
-    for (int k = lane; k < K; k += 64) counts[k] = 0;
-    __syncthreads();
-    if (lane < D) {
-        for (int n = 0; n < N; ++n) {
-            const int c = idv[n];
-            float* s = sums + (int64_t)c * D + lane;
-            *s = fadd(*s, X[(int64_t)n * D + lane]);
-        }
-    } else if (lane == D) {
-        for (int n = 0; n < N; ++n) counts[idv[n]] += 1;
-    }
-    __syncthreads();
-    for (int k = lane; k < K * D; k += 64) {
-        const float fc = (float)(int64_t)(uint32_t)counts[k / D];
-        sums[k] = sums[k] / fc;  // IEEE division; 0/0 = NaN like the DLL
-    }
-}
 
 // ============================================================================
 // KNNScanReduce with exact emulation of ANN's stale kd-tree search.
@@ -606,18 +472,6 @@ __global__ __launch_bounds__(256) void knnfit_kernel(FitFrame* __restrict__ fram
 // launch wrappers (C linkage for the runtime translation unit)
 // ---------------------------------------------------------------------------
 using namespace gsc;
-
-extern "C" hipError_t gsc_launch_yakmo(int D, const ReduceFrame* frames, int nframes, const float* X, float* C,
-                                       float* fs, int* is, uint32_t* bits, hipStream_t st) {
-    dim3 grid(nframes), block(64);
-    switch (D) {
-    case 8: hipLaunchKernelGGL(yakmo_seed_kernel<8>, grid, block, 0, st, frames, nframes, X, C, fs, is, bits); break;
-    case 16: hipLaunchKernelGGL(yakmo_seed_kernel<16>, grid, block, 0, st, frames, nframes, X, C, fs, is, bits); break;
-    case 32: hipLaunchKernelGGL(yakmo_seed_kernel<32>, grid, block, 0, st, frames, nframes, X, C, fs, is, bits); break;
-    default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
 
 extern "C" hipError_t gsc_launch_scan_pass(int D, ReduceFrame* frames, int nframes, int K, const float* X, float* C,
                                            int* is, float* fs, const float* rate_tab, double tol, int pass,

@@ -187,6 +187,8 @@ int run_reduce_batch(int D, int K, int precision, const std::vector<int>& Ns, co
     const int nf = int(Ns.size());
     if (nf == 0) return 0;
     if (D != 8 && D != 16) return fail("KNNScanReduce kernel supports D = 8 or 16 (ChunkSize 4 or 8)");
+    for (int n : Ns)
+        if (n > 262144) return fail("frame has more than 262144 chunks (yakmo seeding bitmap)");
     std::vector<ReduceFrame> fr(static_cast<size_t>(nf));
     int64_t xo = 0, no = 0, maxN = 0;
     for (int i = 0; i < nf; ++i) {
@@ -211,7 +213,7 @@ int run_reduce_batch(int D, int K, int precision, const std::vector<int>& Ns, co
     DevBuf<ReduceFrame> dFr;
     HIP_TRY(dX.alloc(size_t(xo)));
     HIP_TRY(dC.alloc(size_t(nf) * K * D));
-    HIP_TRY(dF.alloc(size_t(no) * 3));
+    HIP_TRY(dF.alloc(size_t(no) * 4));
     HIP_TRY(dI.alloc(size_t(no) + 2 * size_t(nf) * K));
     HIP_TRY(dBits.alloc(size_t(no / 32) + size_t(nf) * 2 + 2));
     HIP_TRY(dFr.alloc(size_t(nf)));
@@ -539,6 +541,7 @@ int gsc_encode_wav(const uint8_t* wav, size_t wav_len, const gsc_options* o, uin
 int gsc_yakmo_seed_means(int n, int d, const float* x, int k, float* centroids) {
     if (ensure_device() != 0) return -1;
     if (k >= n || k <= 0) return fail("yakmo needs 0 < k < n");
+    if (n > 262144) return fail("yakmo seeding supports at most 262144 points");
     std::vector<float> X(x, x + size_t(n) * d), C;
     std::vector<int> cl, it, sl;
     // run only the seeding part: precision 0 => scan loop still runs once; use a
@@ -555,7 +558,7 @@ int gsc_yakmo_seed_means(int n, int d, const float* x, int k, float* centroids) 
     DevBuf<ReduceFrame> dFr;
     HIP_TRY(dX.alloc(X.size()));
     HIP_TRY(dC.alloc(size_t(k) * d));
-    HIP_TRY(dF.alloc(size_t(n) * 3));
+    HIP_TRY(dF.alloc(size_t(n) * 4));
     HIP_TRY(dI.alloc(size_t(n) + size_t(k)));
     HIP_TRY(dBits.alloc(size_t(n / 32) + 4));
     HIP_TRY(dFr.alloc(1));
@@ -585,7 +588,7 @@ int gsc_scan_reduce(int n, int d, const float* x, int k, float* centroids, int* 
     DevBuf<float> dX, dC, dRate, dF;
     DevBuf<int> dI;
     DevBuf<ReduceFrame> dFr;
-    HIP_TRY(dF.alloc(size_t(n) * 3));
+    HIP_TRY(dF.alloc(size_t(n) * 4));
     HIP_TRY(dX.alloc(size_t(n) * d));
     HIP_TRY(dC.alloc(size_t(k) * d));
     HIP_TRY(dI.alloc(size_t(n) + 2 * size_t(k)));

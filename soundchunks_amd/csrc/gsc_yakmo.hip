@@ -1,0 +1,239 @@
+// yakmo k-means++ seeding + seeding means (yakmo_single.dll, called by
+// TFrame.Reduce at encoder.lpr:824-828 as yakmo_create(K,1,0,1,0,0,v)),
+// one workgroup (4 waves) per frame.  Restated from the DLL in SURVEY.md
+// App. C.1 and oracle/yakmo_oracle.c; only the means of the seeding
+// assignment reach the .gsc.
+//
+// Per pick i the DLL walks every point once: d = ((|c|^2 + |x|^2) + 0) -
+// sum_j (2 x_j) c_j (f32, dimension order), keeps the nearest seed (strict
+// <) and, for i < K-1, the running f32 total cum[n] that the next pick's
+// lower_bound searches.  That prefix is one sequential f32 chain per pick;
+// here wave 0 runs it through 64-element registers (readlane + add) while
+// the other waves compute the next block's distances.  Only every 64th cum is
+// stored (a checkpoint); lower_bound replays the chain from the checkpoint
+// below each probe, which reproduces cum exactly (same adds, same order) and
+// therefore the DLL's probe sequence even where tiny negative d make cum
+// non-monotone.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gsc_device.h"
+
+namespace gsc {
+namespace {
+
+__device__ __forceinline__ float fa(float a, float b) { return __fadd_rn(a, b); }
+__device__ __forceinline__ float fs(float a, float b) { return __fsub_rn(a, b); }
+__device__ __forceinline__ float fm(float a, float b) { return __fmul_rn(a, b); }
+
+constexpr int kYThreads = 256;        // 4 waves
+constexpr int kYBits = 262144 / 32;   // chosen-point bitmap in LDS (N <= 262144)
+
+struct YakmoShared {
+    float ring[2][kYThreads];  // d0 of the last two blocks (chain input)
+    uint32_t chosen[kYBits];
+    int cursor[kMaxK];         // stable counting sort of the final assignment
+    float c[32];               // current seed
+    int idx;
+    float total;
+};
+
+// cum[m] of the current pick, replayed from the checkpoint below m (wave 0, all lanes)
+__device__ __forceinline__ float cum_at(const float* __restrict__ d0, const float* __restrict__ ckpt, int m, int lane) {
+    const int blk = m >> 6;
+    float run = blk > 0 ? ckpt[blk - 1] : 0.0f;
+    const float v = d0[(blk << 6) + lane];  // m < N, so the block's first m - 64*blk + 1 loads are in range
+    const int last = m & 63;
+    for (int l = 0; l <= last; ++l) run = fa(run, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)));
+    return run;
+}
+
+}  // namespace
+
+template <int D>
+__global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFrame* __restrict__ frames, int nframes,
+                                                                 const float* __restrict__ Xall, float* __restrict__ Call,
+                                                                 float* __restrict__ f_scratch, int* __restrict__ i_scratch) {
+    __shared__ YakmoShared sh;
+    const int fi = blockIdx.x;
+    if (fi >= nframes) return;
+    const ReduceFrame fr = frames[fi];
+    const int N = fr.N, K = fr.K;
+    const float* __restrict__ X = Xall + fr.x_off;
+    float* C = Call + fr.c_off;
+    float* d0 = f_scratch + fr.n_off * 4;
+    float* norm = d0 + N;
+    float* ckpt = norm + N;          // N/64 + 1 checkpoints
+    int* order = reinterpret_cast<int*>(ckpt + (N >> 6) + 1);  // N point indices (cluster order)
+    int* idv = i_scratch + fr.n_off;  // seeding assignment
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+    // yakmo point norm: norm += v*v (f32, in order) (@0x1800015cb)
+    for (int n = tid; n < N; n += kYThreads) {
+        const float* x = X + (int64_t)n * D;
+        float s = 0.0f;
+#pragma unroll
+        for (int j = 0; j < D; ++j) s = fa(s, fm(x[j], x[j]));
+        norm[n] = s;
+    }
+    for (int w = tid; w < kYBits; w += kYThreads) sh.chosen[w] = 0u;
+    __syncthreads();
+
+    uint64_t rx = 123456789ull, ry = 362436069ull, rz = 521288629ull, rw = 88675123ull;
+    float total = 0.0f;
+    const int nblk = (N + kYThreads - 1) / kYThreads;
+    for (int i = 0; i < K; ++i) {
+        // ---- pick (wave 0; the RNG runs redundantly in every thread)
+        const uint64_t t = rx ^ (rx << 11);
+        rx = ry;
+        ry = rz;
+        rz = rw;
+        rw = rw ^ (rw >> 19) ^ t ^ (t >> 8);
+        const float r = (float)((double)rw * 5.42101086242752217e-20);  // f32(f64(w) * 2^-64)
+        if (wave == 0) {
+            uint32_t idx;
+            if (i == 0) {
+                idx = (uint32_t)(int64_t)floorf(fm(r, (float)N));
+            } else {
+                // std::lower_bound(cum, cum + N, r * total): r*total > cum[mid] moves right
+                const float target = fm(r, total);
+                int first = 0, count = N;
+                while (count > 0) {
+                    const int half = count >> 1;
+                    const int mid = first + half;
+                    if (target > cum_at(d0, ckpt, mid, lane)) {
+                        first = mid + 1;
+                        count -= half + 1;
+                    } else {
+                        count = half;
+                    }
+                }
+                idx = (uint32_t)(int64_t)(float)first;
+            }
+            // collision walk (@0x180001b20) and clamp (@0x180001c50)
+            while (idx < (uint32_t)N && ((sh.chosen[idx >> 5] >> (idx & 31)) & 1u))
+                idx = (idx < (uint32_t)(N - 1)) ? idx + 1 : 0u;
+            if (idx >= (uint32_t)N) idx = (uint32_t)(N - 1);
+            if (lane == 0) {
+                sh.chosen[idx >> 5] |= 1u << (idx & 31);
+                sh.idx = (int)idx;
+            }
+            if (lane < D) sh.c[lane] = X[(int64_t)idx * D + lane];
+        }
+        __syncthreads();
+        const int idx = sh.idx;
+        float c[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) c[j] = sh.c[j];
+        const float cn = norm[idx];
+        const bool chain = i < K - 1;
+        // ---- one pass over the points: d0/id update; wave 0 chains the previous block
+        float run = 0.0f;
+        for (int b = 0; b <= nblk; ++b) {
+            // prefetch this thread's point of block b
+            const int n = b * kYThreads + tid;
+            const bool live = b < nblk && n < N;
+            float xv[D];
+            float xn = 0.0f, dold = 0.0f;
+            if (live) {
+#pragma unroll
+                for (int j = 0; j < D; ++j) xv[j] = X[(int64_t)n * D + j];
+                xn = norm[n];
+                dold = d0[n];
+            }
+            if (wave == 0 && chain && b > 0) {
+                // sequential f32 prefix over block b-1 (encoder's cum[], DLL @0x180001e74)
+                const int base = (b - 1) * kYThreads;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int v = __float_as_int(sh.ring[(b - 1) & 1][k * 64 + lane]);
+                    const int cnt = min(64, N - (base + k * 64));
+                    if (cnt == 64) {
+                        // 64 v_readlane (immediate lanes) into SGPRs, then the dependent adds back to back
+                        int sv[64];
+#pragma unroll
+                        for (int l = 0; l < 64; ++l) sv[l] = __builtin_amdgcn_readlane(v, l);
+#pragma unroll
+                        for (int l = 0; l < 64; ++l) run = fa(run, __int_as_float(sv[l]));
+                    } else {
+                        for (int l = 0; l < cnt; ++l) run = fa(run, __int_as_float(__builtin_amdgcn_readlane(v, l)));
+                    }
+                    if (cnt > 0 && lane == 0) ckpt[((base + k * 64) >> 6)] = run;
+                }
+            }
+            if (live) {
+                float d = fa(fa(cn, xn), 0.0f);
+#pragma unroll
+                for (int j = 0; j < D; ++j) d = fs(d, fm(fa(xv[j], xv[j]), c[j]));
+                float dn = dold;
+                if (i == 0 || dn > d) {
+                    dn = d;
+                    d0[n] = d;
+                    idv[n] = i;
+                }
+                sh.ring[b & 1][tid] = dn;
+            }
+            __syncthreads();
+        }
+        if (wave == 0) total = run;
+    }
+    // ---- means of the seeding assignment (@0x180002290): c = f32(sum in point order) / f32(count)
+    int* counts = i_scratch + fr.k_off;
+    for (int k = tid; k < K; k += kYThreads) sh.cursor[k] = 0;
+    __syncthreads();
+    for (int n = tid; n < N; n += kYThreads) atomicAdd(&sh.cursor[idv[n]], 1);
+    __syncthreads();
+    if (tid == 0) {  // exclusive prefix of the counts
+        int acc = 0;
+        for (int k = 0; k < K; ++k) {
+            const int v = sh.cursor[k];
+            counts[k] = v;
+            sh.cursor[k] = acc;
+            acc += v;
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {  // stable placement: points in index order per cluster
+        for (int base = 0; base < N; base += 64) {
+            const int n = base + lane;
+            const int id = n < N ? idv[n] : -1;
+            const int cnt = min(64, N - base);
+            for (int l = 0; l < cnt; ++l) {
+                const int cl = __builtin_amdgcn_readlane(id, l);
+                if (lane == 0) order[sh.cursor[cl]++] = base + l;
+            }
+        }
+    }
+    __syncthreads();
+    for (int k = tid; k < K; k += kYThreads) {
+        const int cnt = counts[k];
+        const int start = sh.cursor[k] - cnt;
+        float s[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) s[j] = 0.0f;
+        for (int m = 0; m < cnt; ++m) {
+            const float* x = X + (int64_t)order[start + m] * D;
+#pragma unroll
+            for (int j = 0; j < D; ++j) s[j] = fa(s[j], x[j]);
+        }
+        const float fc = (float)(int64_t)(uint32_t)cnt;
+#pragma unroll
+        for (int j = 0; j < D; ++j) C[(int64_t)k * D + j] = s[j] / fc;  // IEEE division; 0/0 = NaN like the DLL
+    }
+}
+
+}  // namespace gsc
+
+using namespace gsc;
+
+extern "C" hipError_t gsc_launch_yakmo(int D, const ReduceFrame* frames, int nframes, const float* X, float* C,
+                                       float* fs, int* is, uint32_t* /*bits*/, hipStream_t st) {
+    dim3 grid(nframes), block(kYThreads);
+    switch (D) {
+    case 8: hipLaunchKernelGGL(yakmo_seed2_kernel<8>, grid, block, 0, st, frames, nframes, X, C, fs, is); break;
+    case 16: hipLaunchKernelGGL(yakmo_seed2_kernel<16>, grid, block, 0, st, frames, nframes, X, C, fs, is); break;
+    case 32: hipLaunchKernelGGL(yakmo_seed2_kernel<32>, grid, block, 0, st, frames, nframes, X, C, fs, is); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
