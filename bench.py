@@ -31,6 +31,8 @@ CONFIGS = {
 }
 
 VALU_F32_PEAK_TOPS = 78.6  # non-fused f32 VALU ops/s: half the 157.3 TFLOPS FMA-counted peak
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md (spec)
+PMC_SUMMARY = ROOT / "profiles" / "r01" / "pmc_summary.json"  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
 
 
 def _dist_env():
@@ -62,7 +64,8 @@ def main():
     ap.add_argument("--seconds", type=float, default=1024.0,
                     help="audio seconds per GPU (1024 s = 256 frames of 4 s: one frame per CU)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--cpu-seconds", type=float, default=1.0, help="oracle baseline sample length")
+    ap.add_argument("--cpu-seconds", type=float, default=1.5,
+                    help="oracle baseline sample: 1.5 s = one 16.5k-chunk frame at the same flags, ~25 s of CPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -76,6 +79,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
     import soundchunks_amd as sc
+    from soundchunks_amd.shard import frame_range, gather_streams
     from soundchunks_amd.synth import synth_wav
 
     if ws > 1:
@@ -86,16 +90,12 @@ def main():
     wav = synth_wav(total_seconds, rate, ch)
     enc = sc.Encoder(argv)
     nframes = enc.frame_count(wav)
-    b = (nframes * rank) // ws
-    e = (nframes * (rank + 1)) // ws
+    b, e = frame_range(nframes, rank, ws)
 
     def step():
         out = enc.encode(wav, b, e)
-        if dist is not None:
-            gathered = [None] * ws if rank == 0 else None
-            dist.gather_object(out, gathered, dst=0)
-            if rank == 0:
-                out = b"".join(gathered)
+        if dist is not None:  # frame-ordered .gsc on rank 0: one padded all-gather (RCCL over xGMI)
+            out = gather_streams(out, device=torch.device("cuda", local))
         return out
 
     for _ in range(args.warmup):
@@ -130,6 +130,14 @@ def main():
     scan_s = tm["gpu_scan_ms"] / 1e3
     launches = max(1, tm["scan_launches"])
     achieved = (ops / scan_s / 1e12) if scan_s > 0 else 0.0
+    avg_launch_s = scan_s / launches
+    # HBM traffic of the scan kernel per launch: PMC bytes per frame (committed
+    # rocprofv3 summary, gfx950-corrected) x frames in this launch
+    traffic = None
+    if PMC_SUMMARY.exists():
+        kern = json.loads(PMC_SUMMARY.read_text())["kernels"].get(f"gsc::scan_batch_kernel<{2 * cs}, 12>")
+        if kern:
+            traffic = kern["hbm_bytes_per_frame_per_launch"] * tm["reduce_frames"]
     result = {
         "metric": "encoded Msamples/s @44.1kHz stereo ChunkSize=8 ChunkCount=4096; bit-exact .gsc",
         "value": round(value, 4),
@@ -146,13 +154,17 @@ def main():
         "config": {"workload": f"{desc}, {total_seconds:g} s synthetic", "frames": nframes, "argv": argv,
                    "parallelism": f"frame-sharded x{ws}"},
         "realtime_x": round(value / (rate * ch / 1e6), 2),
-        "roofline": {"bound": "valu", "kernel": "scan_pass_kernel", "achieved": round(achieved, 4),
-                     "peak": VALU_F32_PEAK_TOPS, "unit": "Tops/s (non-fused f32 VALU)",
-                     "frac": round(achieved / VALU_F32_PEAK_TOPS, 5), "traffic": None,
-                     "avg_launch_ms": round(tm["gpu_scan_ms"] / launches, 3), "ops_per_launch": ops / launches},
+        "roofline": {"bound": "valu", "kernel": "scan_batch_kernel", "achieved": round(achieved, 4),
+                     "peak": VALU_F32_PEAK_TOPS, "unit": "Tops/s (non-fused f32 VALU; bit-exactness rules out FMA/MFMA)",
+                     "frac": round(achieved / VALU_F32_PEAK_TOPS, 5),
+                     "traffic": None if traffic is None else round(traffic),
+                     "hbm_gbs": None if traffic is None else round(traffic / avg_launch_s / 1e9, 2),
+                     "hbm_frac": None if traffic is None else round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 6),
+                     "avg_launch_ms": round(avg_launch_s * 1e3, 3), "ops_per_launch": ops / launches},
         "stages_ms": {k: round(tm[k], 1) for k in ("host_prepare_ms", "host_frames_ms", "gpu_yakmo_ms",
                                                     "gpu_scan_ms", "gpu_knnfit_ms", "host_post_ms", "total_ms")},
-        "scan": {"passes": tm["scan_passes"], "searches": tm["scan_point_passes"], "exact_dfs": tm["scan_slow"]},
+        "scan": {"passes": tm["scan_passes"], "searches": tm["scan_point_passes"], "exact_dfs": tm["scan_slow"],
+                 "solo_resolutions": tm["scan_restarts"]},
     }
     if not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(argv, args.cpu_seconds, rate, ch)

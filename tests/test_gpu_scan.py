@@ -1,0 +1,71 @@
+"""Batched speculative KNNScanReduce (gsc_scan.hip) and yakmo seeding
+(gsc_yakmo.hip) at the benchmark shape K = 4096 / D = 16, against the oracle
+(pytest -m gpu).  Stage parity on a real C2 frame, plus the generic kernel
+forced through the same cases (GSC_SCAN_GENERIC) so both paths stay green.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from golden.cases import CASES
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+@pytest.fixture(scope="module")
+def c2_trace(oracle):
+    make, argv = CASES["syn2s_c2_cs8_cpf4096"]
+    return oracle.trace_frame(make(), argv, 0)
+
+
+def test_yakmo_k4096_bit_exact(c2_trace):
+    import soundchunks_amd as sc
+
+    c = sc.yakmo_seed_means(c2_trace["dataset"], c2_trace["K"])
+    np.testing.assert_array_equal(_bits(c), _bits(c2_trace["yakmo"]))
+
+
+@pytest.mark.parametrize("passes", [1, 3])
+def test_scan_k4096_first_passes(oracle, c2_trace, passes):
+    import soundchunks_amd as sc
+
+    os.environ["GSC_SCAN_MAX_PASSES"] = str(passes)
+    try:
+        gc, gcl, gn = sc.scan_reduce(c2_trace["dataset"], c2_trace["yakmo"], precision=3)
+    finally:
+        del os.environ["GSC_SCAN_MAX_PASSES"]
+    oc, ocl, on = oracle.scan_reduce(c2_trace["dataset"], c2_trace["yakmo"], 3, passes)
+    assert gn == on == passes
+    np.testing.assert_array_equal(gcl, ocl)
+    np.testing.assert_array_equal(_bits(gc), _bits(oc))
+
+
+def test_scan_k4096_full(c2_trace):
+    import soundchunks_amd as sc
+
+    gc, gcl, gn = sc.scan_reduce(c2_trace["dataset"], c2_trace["yakmo"], precision=3)
+    assert gn == c2_trace["scan_iters"]
+    np.testing.assert_array_equal(gcl, c2_trace["clusters"])
+    np.testing.assert_array_equal(_bits(gc), _bits(c2_trace["scan"]))
+
+
+@pytest.mark.parametrize("name", ["hihat_cs8_cpf256", "silence_tone_cs8_cpf256"])
+def test_generic_scan_kernel_still_exact(name):
+    # the generic per-search kernel (non-power-of-2 K, NaN passes) on its own
+    code = (f"import sys; sys.path[:0]=[{str(ROOT)!r},{str(ROOT / 'tests')!r}];"
+            "import soundchunks_amd as sc; from golden.cases import CASES, golden_path;"
+            f"m,a=CASES[{name!r}]; assert sc.Encoder(a).encode(m())==golden_path({name!r}).read_bytes()")
+    env = dict(os.environ, GSC_SCAN_GENERIC="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
