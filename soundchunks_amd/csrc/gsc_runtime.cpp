@@ -610,10 +610,10 @@ int gsc_scan_reduce(int n, int d, const float* x, int k, float* centroids, int* 
     {
         std::fprintf(stderr, "scan: passes %d slow %d restarts %d loop_iters(last pass) %d err %.9g\n", fr[0].iters,
                      fr[0].slow, fr[0].restarts, fr[0].loop_iters, fr[0].err);
-        std::fprintf(stderr, "stamps w0 [S A1 B1 A2 B2 refresh]:");
-        for (int k = 0; k < 6; ++k) std::fprintf(stderr, " %.3g", double(fr[0].stamps[k]));
+        std::fprintf(stderr, "stamps w0 [prep A1 part2rest B2 part3 part4 B1 vcheck won]:");
+        for (int k = 0; k < 10; ++k) std::fprintf(stderr, " %.3g", double(fr[0].stamps[k]));
         std::fprintf(stderr, "\nstamps w1:");
-        for (int k = 6; k < 12; ++k) std::fprintf(stderr, " %.3g", double(fr[0].stamps[k]));
+        for (int k = 10; k < 20; ++k) std::fprintf(stderr, " %.3g", double(fr[0].stamps[k]));
         std::fprintf(stderr, "\n");
     }
     return 0;

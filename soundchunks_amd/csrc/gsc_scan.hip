@@ -104,6 +104,7 @@ struct Scan2Shared {
     int any_nan;
     int st_h[16];      // exact-DFS stack (one lane)
     float st_box[16];
+    uint32_t wkey[2][8];  // parallel exact DFS: per-wave next-improvement keys
 };
 
 #ifdef GSC_STAMPS
@@ -356,31 +357,52 @@ __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const 
 // assuming every query of the batch commits; version table for the checks.
 // Log entry e is lane e: position lg_pos (-1 = empty), tag = committing batch.
 // ---------------------------------------------------------------------------
+// Scan state of one pending query (lane j) / log entry (lane e), built one
+// step per A1 query so the LDS round trips hide under wave 0's distance work.
+struct VPState {
+    int cs, pred, nxt, first, ie;
+};
+
 template <int D, int LOGK>
-__device__ __forceinline__ void v_prepare(Scan2Shared& sh, int qb, int off, int pn, int a1, int lane, int& lg_pos,
-                                          int lg_tag) {
+__device__ __forceinline__ void vp_begin(Scan2Shared& sh, int qb, int off, int pn, int a1, int lane, int& lg_pos,
+                                         int lg_tag, VPState& st) {
     if (lg_pos >= 0 && lg_tag < a1) lg_pos = -1;  // committed before the batch's snapshot
-    const int j = lane;
-    const bool act = j < pn;
-    const QRec& R = sh.qrec[qb][off + (act ? j : 0)];
-    const int cs = act ? R.cstar : -2;
+    st.cs = lane < pn ? sh.qrec[qb][off + lane].cstar : -2;
+    st.pred = -1;
+    st.nxt = kBatch;
+    st.first = kBatch;
+    st.ie = 64;
     sh.vpos[lane] = lg_pos;
     sh.vfrom[lane] = 0;
     wave_lds_sync();
-    int pred = -1, nxt = kBatch, first = kBatch;
-    for (int k = 0; k < pn; ++k) {
-        const int ck = sh.qrec[qb][off + k].cstar;
-        if (k < j && ck == cs) pred = 64 + k;
-        if (k > j && ck == cs && nxt == kBatch) nxt = k;
-        if (ck == lg_pos && first == kBatch) first = k;  // lane as log entry: first query moving it
-    }
-    // log entry holding c*_j (c*_j moved before the batch)
-    int ie = -1;
-    for (int e = 63; e >= 0; --e)
-        if (sh.vpos[e] == cs) ie = e;
-    if (pred < 0) pred = ie;
+}
+
+// step k: pending query k against every lane's query / entry; log entries 2k, 2k+1
+__device__ __forceinline__ void vp_step(const Scan2Shared& sh, int qb, int off, int pn, int k, int lane, int lg_pos,
+                                        VPState& st) {
+    const int ck = k < pn ? sh.qrec[qb][off + k].cstar : -3;
+    if (k < lane && ck == st.cs) st.pred = 64 + k;
+    if (k > lane && ck == st.cs && st.nxt == kBatch) st.nxt = k;
+    if (ck == lg_pos && st.first == kBatch) st.first = k;  // lane as log entry: first query moving it
+    if (sh.vpos[2 * k] == st.cs) st.ie = min(st.ie, 2 * k);
+    if (sh.vpos[2 * k + 1] == st.cs) st.ie = min(st.ie, 2 * k + 1);
+}
+
+// Commit, step 1 (wave 0, lanes = queries j of the pending batch): online
+// updates in order per centroid (encoder.lpr:735-740, f32 c += (x - c) * rate)
+// assuming every query of the batch commits; version table for the checks.
+// Log entry e is lane e: position lg_pos (-1 = empty), tag = commit iteration.
+template <int D, int LOGK>
+__device__ __forceinline__ void vp_end(Scan2Shared& sh, int qb, int off, int pn, int lane, int lg_pos,
+                                       const VPState& st) {
+    const int j = lane;
+    const bool act = j < pn;
+    const QRec& R = sh.qrec[qb][off + (act ? j : 0)];
+    const int cs = st.cs, nxt = st.nxt;
+    const int ie = st.ie < 64 ? st.ie : -1;  // log entry holding c*_j (c*_j moved before the batch)
+    const int pred = st.pred >= 0 ? st.pred : ie;
     // versions: log entries (0..63) and "after query j" (64+j)
-    sh.vto[lane] = lg_pos >= 0 ? first : -1;
+    sh.vto[lane] = lg_pos >= 0 ? st.first : -1;
     if (lane < kBatch) {
         sh.vpos[64 + lane] = act ? cs : -1;
         sh.vfrom[64 + lane] = j + 1;
@@ -516,6 +538,115 @@ __device__ __forceinline__ void dfs_exact(Scan2Shared& sh, int tid, int nthreads
     lds_barrier();
 }
 
+// Exact ANN ann_search (k = 1, eps = 0; annkSearch @0x1800124b0), all
+// threads: the result of the stale-tree DFS is decided by its strict
+// improvements only.  With leaves ranked in near-first DFS order, a leaf is
+// reached while the best distance is b iff every far subtree on its path
+// entered after the current best was found has box' < b; box' only grows
+// along a path, so that is one test on its innermost far subtree (start rank
+// s*, box' bx*).  The next improvement is the lowest-ranked reached leaf with
+// d < b, found by one block min-reduction per improvement.  Live leaf
+// distances come from sh.dist.
+template <int D, int LOGK, int NW>
+__device__ __forceinline__ void dfs_parallel(Scan2Shared& sh, int tid, int lane, int wave, int& out_pos, float& out_key) {
+    constexpr int K = 1 << LOGK;
+    constexpr int nthreads = 64 * NW;
+    const float* q = sh.qslow;
+    for (int h = tid; h < K - 1; h += nthreads) {  // split nodes: box' increment, sign = near child hi
+        const int cdim = sh.t.cd[h];
+        const float qc = q[cdim];
+        const float cut = fsub(qc, sh.t.cv[h]);
+        const bool nearlo = cut < 0.0f;
+        float bd = nearlo ? fsub(sh.t.lo[h], qc) : fsub(qc, sh.t.hi[h]);
+        if (bd < 0.0f) bd = 0.0f;
+        const float inc = fsub(fmul(cut, cut), fmul(bd, bd));  // >= +0
+        sh.dfs_inc[h] = nearlo ? inc : -inc;
+    }
+    float rootbox = 0.0f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {  // annBoxDistance
+        const float qd = q[d];
+        if (sh.t.bnd_lo[d] > qd) {
+            const float t = fsub(sh.t.bnd_lo[d], qd);
+            rootbox = fadd(rootbox, fmul(t, t));
+        } else if (qd > sh.t.bnd_hi[d]) {
+            const float t = fsub(qd, sh.t.bnd_hi[d]);
+            rootbox = fadd(rootbox, fmul(t, t));
+        }
+    }
+    lds_barrier();
+    // this lane's 8 leaves (an aligned depth LOGK-3 subtree): DFS rank, start
+    // rank and box' of the innermost far subtree (-1 / none if all-near)
+    const int p0 = tid * 8;
+    int rs[8];  // rank << 13 | (s* + 1)
+    float bxs[8];
+    {
+        float box = rootbox, bF = 0.0f;
+        int pref = 0, sF = -1, h = 0;
+        for (int l = 0; l < LOGK - 3; ++l) {
+            const int bit = (p0 >> (LOGK - 1 - l)) & 1;
+            const float v = sh.dfs_inc[h];
+            if (bit != (int)(__float_as_uint(v) >> 31)) {
+                box = fadd(box, fabsf(v));
+                sF = pref + (1 << (LOGK - 1 - l));
+                bF = box;
+                pref += 1 << (LOGK - 1 - l);
+            }
+            h = 2 * h + 1 + bit;
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            float box2 = box, bF2 = bF;
+            int pref2 = pref, sF2 = sF, h2 = h;
+#pragma unroll
+            for (int l = LOGK - 3; l < LOGK; ++l) {
+                const int bit = ((p0 + s) >> (LOGK - 1 - l)) & 1;
+                const float v = sh.dfs_inc[h2];
+                if (bit != (int)(__float_as_uint(v) >> 31)) {
+                    box2 = fadd(box2, fabsf(v));
+                    sF2 = pref2 + (1 << (LOGK - 1 - l));
+                    bF2 = box2;
+                    pref2 += 1 << (LOGK - 1 - l);
+                }
+                h2 = 2 * h2 + 1 + bit;
+            }
+            rs[s] = (pref2 << 13) | (sF2 + 1);
+            bxs[s] = bF2;
+        }
+    }
+    // improvements: the empty list takes the first leaf reached (max_key = FLT_MAX)
+    int pos = -1, bp = -1, par = 0;
+    float b = FLT_MAX;
+    for (;;) {
+        uint32_t key = 0xFFFFFFFFu;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const int rk = rs[s] >> 13, st = (rs[s] & 8191) - 1;
+            const bool reach = st <= pos || bxs[s] < b;
+            if (p0 + s < K && rk > pos && reach && sh.dist[p0 + s] < b)
+                key = min(key, ((uint32_t)rk << 12) | (uint32_t)(p0 + s));
+        }
+        key = min(key, partner<0>(key));
+        key = min(key, partner<1>(key));
+        key = min(key, partner<2>(key));
+        key = min(key, partner<3>(key));
+        key = min(key, partner<4>(key));
+        key = min((uint32_t)__builtin_amdgcn_readlane((int)key, 0), (uint32_t)__builtin_amdgcn_readlane((int)key, 32));
+        if (lane == 0) sh.wkey[par][wave] = key;
+        lds_barrier();
+        uint32_t g = 0xFFFFFFFFu;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) g = min(g, sh.wkey[par][w]);
+        par ^= 1;
+        if (g == 0xFFFFFFFFu) break;
+        pos = (int)(g >> 12);
+        bp = (int)(g & 4095u);
+        b = sh.dist[bp];
+    }
+    out_pos = bp;
+    out_key = b;
+}
+
 // fold published log entries into the owners' registers
 template <int D>
 __device__ __forceinline__ void refresh(Scan2Shared& sh, float (&creg)[8][D], int wave, int lane) {
@@ -604,7 +735,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
     double err = 0.0;
     int slow_total = 0, restarts = 0;
 #ifdef GSC_STAMPS
-    uint64_t acc[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tlast = stamp();
 #endif
     // batches awaiting commit, in order: buffer, first query of the buffer,
@@ -625,14 +756,25 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
             pre[e] = (k < kBatch * D && next_load + k / D < N) ? X[(int64_t)next_load * D + k] : 0.0f;
         }
         // ---- part 1: chain the pending batch's updates (wave 0); A1(current)
-        if (wave == 0 && has_p) v_prepare<D, LOGK>(sh, P_buf, P_off, P_n, vq_a1[0], lane, lg_pos, lg_tag);
+        VPState vst;
+        if (wave == 0 && has_p) vp_begin<D, LOGK>(sh, P_buf, P_off, P_n, vq_a1[0], lane, lg_pos, lg_tag, vst);
         STAMP(0)
 #pragma unroll 1
-        for (int jj = 0; jj < cur_n; ++jj) a1_query<D, LOGK>(creg, sh.q[cur_buf][jj], sh.wrec[wave][jj], wave, lane);
+        for (int jj = 0; jj < cur_n; ++jj) {
+            a1_query<D, LOGK>(creg, sh.q[cur_buf][jj], sh.wrec[wave][jj], wave, lane);
+            if (wave == 0 && has_p) vp_step(sh, P_buf, P_off, P_n, jj, lane, lg_pos, vst);
+        }
+        if (wave == 0 && has_p) {
+#pragma unroll 1
+            for (int k = cur_n; k < kBatch; ++k) vp_step(sh, P_buf, P_off, P_n, k, lane, lg_pos, vst);
+            vp_end<D, LOGK>(sh, P_buf, P_off, P_n, lane, lg_pos, vst);
+        }
         STAMP(1)
         lds_barrier();
+        STAMP(6)
         // ---- part 2: check the pending batch; certificates of the current batch
         if (has_p) v_check<D, LOGK>(sh, P_buf, P_off, P_n, tid, nthreads);
+        STAMP(7)
         if (cur_n > 0) {
             // c*'s snapshot coordinates, written by the wave that owns c*
             uint64_t won;
@@ -662,6 +804,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
                         for (int d = 0; d < D; ++d) sh.qrec[cur_buf][jj].o[d] = creg[s][d];
                     }
             }
+            STAMP(8)
 #pragma unroll 1
             for (int j0 = wave * 4; j0 < cur_n; j0 += 4 * NW)
                 a2_group<D, LOGK, NW>(sh, j0, cur_n, sh.q[cur_buf], sh.qrec[cur_buf], 0, lane);
@@ -792,9 +935,27 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
 #pragma unroll
                 for (int s = 0; s < 8; ++s)
                     if (p0 + s < K) sh.dist[p0 + s] = dv[s];
-                dfs_exact<D, LOGK>(sh, tid, nthreads);
-                bpos = uniform_int(sh.slow_pos);
-                key = sh.slow_key;
+                // the centroid registers wait in C (pass-start copy, rewritten at pass end)
+                // so the DFS has the register file
+#pragma unroll
+                for (int s = 0; s < 8; ++s)
+                    if (p0 + s < K) {
+                        const int id = sh.t.pidx[p0 + s];
+#pragma unroll
+                        for (int d = 0; d < D; ++d) C[(int64_t)id * D + d] = creg[s][d];
+                    }
+                __asm__ volatile("" ::: "memory");  // the reload below must not be forwarded from the stores
+                lds_barrier();  // sh.dist complete
+                dfs_parallel<D, LOGK, NW>(sh, tid, lane, wave, bpos, key);
+                bpos = uniform_int(bpos);
+                __asm__ volatile("" ::: "memory");
+#pragma unroll
+                for (int s = 0; s < 8; ++s)
+                    if (p0 + s < K) {
+                        const int id = sh.t.pidx[p0 + s];
+#pragma unroll
+                        for (int d = 0; d < D; ++d) creg[s][d] = C[(int64_t)id * D + d];
+                    }
                 ++slow_total;
             }
             // owner publishes c's coordinates; tid 0 moves it (encoder.lpr:735-744);
@@ -857,7 +1018,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
     }
 #ifdef GSC_STAMPS
     if (lane == 0 && wave < 2)
-        for (int k = 0; k < 6; ++k) frp->stamps[wave * 6 + k] += acc[k];
+        for (int k = 0; k < 10; ++k) frp->stamps[wave * 10 + k] += acc[k];
 #endif
     if (tid == 0) {
         const double prev_err = pass == 0 ? 3.4028234663852886e+38 : frp->err;  // err := MaxSingle
