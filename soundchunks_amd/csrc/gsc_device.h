@@ -29,7 +29,9 @@ struct ReduceFrame {
     int32_t generic;      // this pass needs the generic kernel (NaN centroids)
     int32_t restarts;     // out: batched-pipeline restarts (diagnostic)
     int32_t loop_iters;   // out: batched-pipeline iterations (diagnostic); -1 = guard tripped
-    uint64_t stamps[20];  // out (GSC_STAMPS builds only): per-phase cycles, waves 0 and 1
+    int32_t tree_exact;   // out: passes whose kd-tree needed the sequential build (median ties)
+    int32_t pad_;
+    uint64_t stamps[96];  // out (GSC_STAMPS builds only): per-phase cycles, 12 per wave
 };
 
 // One frame of TFrame.KNNFit (encoder.lpr:915-978).

@@ -608,12 +608,13 @@ int gsc_scan_reduce(int n, int d, const float* x, int k, float* centroids, int* 
     if (fr[0].loop_iters < 0) return fail("KNNScanReduce: batched pipeline made no progress (guard tripped)");
     if (std::getenv("GSC_SCAN_DEBUG"))
     {
-        std::fprintf(stderr, "scan: passes %d slow %d restarts %d loop_iters(last pass) %d err %.9g\n", fr[0].iters,
-                     fr[0].slow, fr[0].restarts, fr[0].loop_iters, fr[0].err);
-        std::fprintf(stderr, "stamps w0 [prep A1 part2rest B2 part3 part4 B1 vcheck won]:");
-        for (int k = 0; k < 10; ++k) std::fprintf(stderr, " %.3g", double(fr[0].stamps[k]));
-        std::fprintf(stderr, "\nstamps w1:");
-        for (int k = 10; k < 20; ++k) std::fprintf(stderr, " %.3g", double(fr[0].stamps[k]));
+        std::fprintf(stderr, "scan: passes %d slow %d restarts %d loop_iters(last pass) %d err %.9g tree_exact %d\n",
+                     fr[0].iters, fr[0].slow, fr[0].restarts, fr[0].loop_iters, fr[0].err, fr[0].tree_exact);
+        std::fprintf(stderr, "stamps [prep A1 vcheck B2 part3 part4 B1 vpend wonA2 setup soloA soloDFS]");
+        for (int w = 0; w < 8; ++w) {
+            std::fprintf(stderr, "\n  w%d:", w);
+            for (int k = 0; k < 12; ++k) std::fprintf(stderr, " %.3g", double(fr[0].stamps[w * 12 + k]));
+        }
         std::fprintf(stderr, "\n");
     }
     return 0;

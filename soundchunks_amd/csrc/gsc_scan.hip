@@ -180,13 +180,9 @@ __device__ __forceinline__ float seqdist(const float* __restrict__ a, const floa
 // ---------------------------------------------------------------------------
 // A1: snapshot distances of one query against this wave's 512 leaves.
 // ---------------------------------------------------------------------------
-template <int D, int LOGK>
-__device__ __forceinline__ void a1_query(const float (&creg)[8][D], const float* __restrict__ qv, WaveRec& rec,
-                                         int wave, int lane) {
-    constexpr int K = 1 << LOGK;
-    const int p0 = (wave * 64 + lane) * 8;
+template <int D>
+__device__ __forceinline__ void a1_dist(const float (&creg)[8][D], const float* __restrict__ qv, float (&dv)[8]) {
     // ANN leaf distance (ANN.dll @0x1800128b0): dist = dist + (q[d]-p[d])^2, d = 0..D-1
-    float dv[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) dv[s] = 0.0f;
 #pragma unroll
@@ -198,8 +194,15 @@ __device__ __forceinline__ void a1_query(const float (&creg)[8][D], const float*
             dv[s] = fadd(dv[s], fmul(t, t));
         }
     }
+}
+
+// wave min-tree over the lanes' 8 leaf distances -> the query's WaveRec
+template <int LOGK>
+__device__ __forceinline__ void a1_reduce(const float (&dv)[8], WaveRec& rec, int wave, int lane) {
+    constexpr int K = 1 << LOGK;
+    const int p0 = (wave * 64 + lane) * 8;
     uint32_t b[8];
-    const bool has = p0 < K;
+    const bool has = LOGK >= 9 || p0 < K;  // K >= 512: every lane holds 8 leaves
 #pragma unroll
     for (int s = 0; s < 8; ++s) b[s] = has ? __float_as_uint(dv[s]) : 0xFFFFFFFFu;
     const uint32_t m01 = min(b[0], b[1]), m23 = min(b[2], b[3]), m45 = min(b[4], b[5]), m67 = min(b[6], b[7]);
@@ -215,11 +218,14 @@ __device__ __forceinline__ void a1_query(const float (&creg)[8][D], const float*
     v = min(v, sl2);
     const uint32_t sl3 = partner<3>(v);
     v = min(v, sl3);
-    const uint32_t sl4 = partner<4>(v);
-    v = min(v, sl4);
-    const uint32_t vlo = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
-    const uint32_t vhi = (uint32_t)__builtin_amdgcn_readlane((int)v, 32);
-    const uint32_t wmin = min(vlo, vhi);
+    // the two widest levels with the gfx950 row / half swaps: p[0] is this
+    // lane's copy of the lower row (half), p[1] of the upper one
+    const auto p16 = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    const uint32_t sl4 = (lane & 16) ? p16[0] : p16[1];
+    v = min(p16[0], p16[1]);
+    const auto p32 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    const uint32_t sl5 = (lane & 32) ? p32[0] : p32[1];
+    const uint32_t wmin = min(p32[0], p32[1]);
     const uint64_t m = __ballot(lmin == wmin);
     const int L = __ffsll((long long)m) - 1;
     if (lane == L) {
@@ -241,11 +247,19 @@ __device__ __forceinline__ void a1_query(const float (&creg)[8][D], const float*
         rec.sib[2] = sl2;
         rec.sib[3] = sl3;
         rec.sib[4] = sl4;
-        rec.sib[5] = lane < 32 ? vhi : vlo;
+        rec.sib[5] = sl5;
         rec.sib[6] = (ls & 1) ? pa : pb;
         rec.sib[7] = (ls & 4) ? ((ls & 2) ? m45 : m67) : ((ls & 2) ? m01 : m23);
         rec.sib[8] = (ls & 4) ? m03 : m47;
     }
+}
+
+template <int D, int LOGK>
+__device__ __forceinline__ void a1_query(const float (&creg)[8][D], const float* __restrict__ qv, WaveRec& rec,
+                                         int wave, int lane) {
+    float dv[8];
+    a1_dist<D>(creg, qv, dv);
+    a1_reduce<LOGK>(dv, rec, wave, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -692,11 +706,17 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nthreads = 64 * NW;
 
+#ifdef GSC_STAMPS
+    const uint64_t t_kernel0 = stamp();
+#endif
     if (pass == 0)
         for (int k = tid; k < K; k += nthreads) prev_cnt[k] = 1;  // CCntStart (encoder.lpr:717-721)
     if (tid == 0) sh.any_nan = 0;
     __syncthreads();
-    build_tree<D>(sh.t, sh.dist, C, K);
+    if (!build_tree_fast<D, LOGK, 64 * NW>(sh.t, sh.dist, sh.dfs_inc, C, &sh.slow_pos)) {
+        build_tree<D>(sh.t, sh.dist, C, K);  // median ties: quickselect's exact order
+        if (tid == 0) frp->tree_exact += 1;
+    }
 
     float creg[8][D];
     const int p0 = tid * 8;
@@ -735,8 +755,9 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
     double err = 0.0;
     int slow_total = 0, restarts = 0;
 #ifdef GSC_STAMPS
-    uint64_t acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tlast = stamp();
+    acc[9] = tlast - t_kernel0;  // pass setup: tree build, registers, first queries
 #endif
     // batches awaiting commit, in order: buffer, first query of the buffer,
     // first uncommitted slot, count, iteration of their distance snapshot
@@ -916,6 +937,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
             lds_barrier();
             int bpos;
             float key;
+            STAMP(10)
             if (uniform_int(sh.qsolo.valid)) {
                 bpos = uniform_int(sh.qsolo.cstar);
                 key = sh.qsolo.g;
@@ -957,6 +979,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
                         for (int d = 0; d < D; ++d) creg[s][d] = C[(int64_t)id * D + d];
                     }
                 ++slow_total;
+                STAMP(11)
             }
             // owner publishes c's coordinates; tid 0 moves it (encoder.lpr:735-744);
             // the move enters the log (later batches' snapshots miss it) and the registers
@@ -1018,7 +1041,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
     }
 #ifdef GSC_STAMPS
     if (lane == 0 && wave < 2)
-        for (int k = 0; k < 10; ++k) frp->stamps[wave * 10 + k] += acc[k];
+        for (int k = 0; k < 12; ++k) frp->stamps[wave * 12 + k] += acc[k];
 #endif
     if (tid == 0) {
         const double prev_err = pass == 0 ? 3.4028234663852886e+38 : frp->err;  // err := MaxSingle

@@ -36,6 +36,185 @@ struct KdTree {
     float bnd_lo[32], bnd_hi[32];  // annEnclRect of the pass's centroids
 };
 
+// ---------------------------------------------------------------------------
+// Parallel build for K = 2^LOGK (the batched scan kernel).  ANN's build is
+// order dependent only through ties: annMaxSpread's min/max, the median's
+// left set (the n_lo smallest cut values) and the cut value (max of the left
+// set + min of the right set) / 2 are functions of each node's point SET as
+// long as the two values at the median boundary differ.  Then the children's
+// sets, and by induction the whole tree and its leaf order, do not depend on
+// the order quickselect leaves inside a segment.  So each level: per-node
+// spreads by reductions, cut values gathered, every segment bitonic-sorted in
+// LDS, the left half taken.  A node whose boundary values tie (or compare
+// unordered) makes the function return false: the caller then runs the
+// sequential build_tree, which reproduces quickselect's tie order exactly.
+//   val: K floats of LDS scratch; red: 2*D*(K/512) floats of LDS scratch.
+// ---------------------------------------------------------------------------
+template <int D, int LOGK, int NT>
+__device__ bool build_tree_fast(KdTree& t, float* __restrict__ val, float* __restrict__ red,
+                                const float* __restrict__ C, int* tie) {
+    constexpr int K = 1 << LOGK;
+    constexpr int PT = K / NT;  // kd-leaf positions per thread
+    static_assert(PT * NT == K && (PT == 4 || PT == 8), "positions per thread");
+    const int tid = threadIdx.x, wave = tid >> 6;
+    const int p0 = tid * PT;
+    for (int p = tid; p < K; p += NT) t.pidx[p] = (uint16_t)p;
+    if (tid == 0) *tie = 0;
+    __syncthreads();
+    for (int L = 0; L < LOGK; ++L) {
+        const int S = K >> L;  // segment (node) size at this level
+        const int first = (1 << L) - 1;
+        // ---- annMaxSpread per node: min / max per dimension -> cut dimension
+        if (S >= PT) {
+            float mn[D], mx[D];
+            {
+                const float* r = C + (int64_t)t.pidx[p0] * D;
+#pragma unroll
+                for (int d = 0; d < D; ++d) mn[d] = mx[d] = r[d];
+            }
+#pragma unroll
+            for (int i = 1; i < PT; ++i) {
+                const float* r = C + (int64_t)t.pidx[p0 + i] * D;
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    const float c = r[d];
+                    mn[d] = fminf(mn[d], c);
+                    mx[d] = fmaxf(mx[d], c);
+                }
+            }
+            const int G = S / PT;  // threads per node
+            const int GW = G < 64 ? G : 64;
+            for (int o = 1; o < GW; o <<= 1) {
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    mn[d] = fminf(mn[d], __shfl_xor(mn[d], o));
+                    mx[d] = fmaxf(mx[d], __shfl_xor(mx[d], o));
+                }
+            }
+            if (G > 64) {  // node spans G/64 waves
+                if ((tid & 63) == 0) {
+#pragma unroll
+                    for (int d = 0; d < D; ++d) {
+                        red[wave * 2 * D + d] = mn[d];
+                        red[wave * 2 * D + D + d] = mx[d];
+                    }
+                }
+                __syncthreads();
+                const int wn = G / 64, w0 = (wave / wn) * wn;
+                for (int w = w0; w < w0 + wn; ++w) {
+#pragma unroll
+                    for (int d = 0; d < D; ++d) {
+                        mn[d] = fminf(mn[d], red[w * 2 * D + d]);
+                        mx[d] = fmaxf(mx[d], red[w * 2 * D + D + d]);
+                    }
+                }
+            }
+            if (p0 % S == 0) {
+                int cdim = 0;
+                float max_spr = 0.0f;
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    const float spr = fsub(mx[d], mn[d]);
+                    if (spr > max_spr) {
+                        max_spr = spr;
+                        cdim = d;
+                    }
+                }
+                t.cd[first + p0 / S] = (uint8_t)cdim;
+                if (L == 0) {  // annEnclRect of all centroids
+#pragma unroll
+                    for (int d = 0; d < D; ++d) {
+                        t.bnd_lo[d] = mn[d];
+                        t.bnd_hi[d] = mx[d];
+                    }
+                }
+            }
+        } else {  // several nodes per thread
+            for (int g = 0; g < PT / S; ++g) {
+                float mn[D], mx[D];
+                const int pb = p0 + g * S;
+                {
+                    const float* r = C + (int64_t)t.pidx[pb] * D;
+#pragma unroll
+                    for (int d = 0; d < D; ++d) mn[d] = mx[d] = r[d];
+                }
+                for (int i = 1; i < S; ++i) {
+                    const float* r = C + (int64_t)t.pidx[pb + i] * D;
+#pragma unroll
+                    for (int d = 0; d < D; ++d) {
+                        const float c = r[d];
+                        mn[d] = fminf(mn[d], c);
+                        mx[d] = fmaxf(mx[d], c);
+                    }
+                }
+                int cdim = 0;
+                float max_spr = 0.0f;
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    const float spr = fsub(mx[d], mn[d]);
+                    if (spr > max_spr) {
+                        max_spr = spr;
+                        cdim = d;
+                    }
+                }
+                t.cd[first + pb / S] = (uint8_t)cdim;
+            }
+        }
+        __syncthreads();
+        // ---- cut-dimension values of every position
+#pragma unroll
+        for (int i = 0; i < PT; ++i) {
+            const int p = p0 + i;
+            val[p] = C[(int64_t)t.pidx[p] * D + t.cd[first + p / S]];
+        }
+        __syncthreads();
+        // ---- bitonic sort of every segment (ascending; order among equal values is free)
+        for (int k = 2; k <= S; k <<= 1) {
+            for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+                for (int e = 0; e < PT / 2; ++e) {
+                    const int i = tid + e * NT;
+                    const int a = ((i & ~(j - 1)) << 1) | (i & (j - 1));
+                    const int b = a + j;
+                    const bool up = k == S || (a & k) == 0;
+                    const float va = val[a], vb = val[b];
+                    if (up ? (va > vb) : (va < vb)) {
+                        val[a] = vb;
+                        val[b] = va;
+                        const uint16_t ia = t.pidx[a];
+                        t.pidx[a] = t.pidx[b];
+                        t.pidx[b] = ia;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        // ---- per node: cut value, tie check, cell bounds on the cut dimension
+        for (int node = tid; node < (1 << L); node += NT) {
+            const int h = first + node, s = node * S, nl = S >> 1;
+            const float a = val[s + nl - 1], b = val[s + nl];
+            if (!(a < b)) *tie = 1;
+            const int cdim = t.cd[h];
+            float lov = t.bnd_lo[cdim], hiv = t.bnd_hi[cdim];
+            int an = 0;
+            const int path = h + 1;
+            for (int bl = L - 1; bl >= 0; --bl) {
+                const int right = (path >> bl) & 1;
+                if (t.cd[an] == cdim) {
+                    if (right) lov = t.cv[an];
+                    else hiv = t.cv[an];
+                }
+                an = 2 * an + 1 + right;
+            }
+            t.cv[h] = (float)((double)fadd(a, b) / 2.0);
+            t.lo[h] = lov;
+            t.hi[h] = hiv;
+        }
+        __syncthreads();
+    }
+    return *tie == 0;
+}
+
 // segment of heap node h (root 0, children 2h+1 / 2h+2, n_lo = n/2)
 __device__ __forceinline__ void node_segment(int h, int K, int& s, int& n, int& depth) {
     s = 0;
