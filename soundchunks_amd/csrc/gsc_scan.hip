@@ -1040,7 +1040,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
         }
     }
 #ifdef GSC_STAMPS
-    if (lane == 0 && wave < 2)
+    if (lane == 0)
         for (int k = 0; k < 12; ++k) frp->stamps[wave * 12 + k] += acc[k];
 #endif
     if (tid == 0) {

@@ -14,6 +14,11 @@
 // below each probe, which reproduces cum exactly (same adds, same order) and
 // therefore the DLL's probe sequence even where tiny negative d make cum
 // non-monotone.
+//
+// Roles: wave 0 only picks and chains (the prefix is the critical path, one
+// dependent f32 add per point); waves 1..4 compute the distances of one
+// 256-point block per step, with the next block's loads issued a step ahead so
+// HBM latency hides under the chain.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -26,11 +31,12 @@ __device__ __forceinline__ float fa(float a, float b) { return __fadd_rn(a, b); 
 __device__ __forceinline__ float fs(float a, float b) { return __fsub_rn(a, b); }
 __device__ __forceinline__ float fm(float a, float b) { return __fmul_rn(a, b); }
 
-constexpr int kYThreads = 256;        // 4 waves
+constexpr int kYBlock = 256;          // points per pipeline step (waves 1..4)
+constexpr int kYThreads = 64 + kYBlock;  // wave 0: picks + prefix chain
 constexpr int kYBits = 262144 / 32;   // chosen-point bitmap in LDS (N <= 262144)
 
 struct YakmoShared {
-    float ring[2][kYThreads];  // d0 of the last two blocks (chain input)
+    float ring[2][kYBlock];    // d0 of the last two blocks (chain input)
     uint32_t chosen[kYBits];
     int cursor[kMaxK];         // stable counting sort of the final assignment
     float c[32];               // current seed
@@ -81,7 +87,8 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
 
     uint64_t rx = 123456789ull, ry = 362436069ull, rz = 521288629ull, rw = 88675123ull;
     float total = 0.0f;
-    const int nblk = (N + kYThreads - 1) / kYThreads;
+    const int nblk = (N + kYBlock - 1) / kYBlock;
+    const int dt = tid - 64;  // distance thread of waves 1..4 (negative on wave 0)
     for (int i = 0; i < K; ++i) {
         // ---- pick (wave 0; the RNG runs redundantly in every thread)
         const uint64_t t = rx ^ (rx << 11);
@@ -121,61 +128,71 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
             if (lane < D) sh.c[lane] = X[(int64_t)idx * D + lane];
         }
         __syncthreads();
-        const int idx = sh.idx;
-        float c[D];
-#pragma unroll
-        for (int j = 0; j < D; ++j) c[j] = sh.c[j];
-        const float cn = norm[idx];
         const bool chain = i < K - 1;
-        // ---- one pass over the points: d0/id update; wave 0 chains the previous block
-        float run = 0.0f;
-        for (int b = 0; b <= nblk; ++b) {
-            // prefetch this thread's point of block b
-            const int n = b * kYThreads + tid;
-            const bool live = b < nblk && n < N;
+        if (wave == 0) {
+            // sequential f32 prefix over the blocks as they complete (encoder's cum[], DLL @0x180001e74)
+            float run = 0.0f;
+            for (int b = 0; b <= nblk; ++b) {
+                if (chain && b > 0) {
+                    const int base = (b - 1) * kYBlock;
+#pragma unroll
+                    for (int k = 0; k < kYBlock / 64; ++k) {
+                        const int v = __float_as_int(sh.ring[(b - 1) & 1][k * 64 + lane]);
+                        const int cnt = min(64, N - (base + k * 64));
+                        if (cnt == 64) {
+                            // 64 v_readlane (immediate lanes) into SGPRs, then the dependent adds back to back
+                            int sv[64];
+#pragma unroll
+                            for (int l = 0; l < 64; ++l) sv[l] = __builtin_amdgcn_readlane(v, l);
+#pragma unroll
+                            for (int l = 0; l < 64; ++l) run = fa(run, __int_as_float(sv[l]));
+                        } else {
+                            for (int l = 0; l < cnt; ++l) run = fa(run, __int_as_float(__builtin_amdgcn_readlane(v, l)));
+                        }
+                        if (cnt > 0 && lane == 0) ckpt[((base + k * 64) >> 6)] = run;
+                    }
+                }
+                __syncthreads();
+            }
+            total = run;
+        } else {
+            float c[D];
+#pragma unroll
+            for (int j = 0; j < D; ++j) c[j] = sh.c[j];
+            const float cn = norm[sh.idx];
+            // one pass over the points: d0/id update, block b+1 prefetched during step b
             float xv[D];
             float xn = 0.0f, dold = 0.0f;
-            if (live) {
+            if (dt < N) {
 #pragma unroll
-                for (int j = 0; j < D; ++j) xv[j] = X[(int64_t)n * D + j];
-                xn = norm[n];
-                dold = d0[n];
+                for (int j = 0; j < D; ++j) xv[j] = X[(int64_t)dt * D + j];
+                xn = norm[dt];
+                dold = d0[dt];
             }
-            if (wave == 0 && chain && b > 0) {
-                // sequential f32 prefix over block b-1 (encoder's cum[], DLL @0x180001e74)
-                const int base = (b - 1) * kYThreads;
+            for (int b = 0; b <= nblk; ++b) {
+                const int n = b * kYBlock + dt;
+                if (b < nblk && n < N) {
+                    float d = fa(fa(cn, xn), 0.0f);
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int v = __float_as_int(sh.ring[(b - 1) & 1][k * 64 + lane]);
-                    const int cnt = min(64, N - (base + k * 64));
-                    if (cnt == 64) {
-                        // 64 v_readlane (immediate lanes) into SGPRs, then the dependent adds back to back
-                        int sv[64];
-#pragma unroll
-                        for (int l = 0; l < 64; ++l) sv[l] = __builtin_amdgcn_readlane(v, l);
-#pragma unroll
-                        for (int l = 0; l < 64; ++l) run = fa(run, __int_as_float(sv[l]));
-                    } else {
-                        for (int l = 0; l < cnt; ++l) run = fa(run, __int_as_float(__builtin_amdgcn_readlane(v, l)));
+                    for (int j = 0; j < D; ++j) d = fs(d, fm(fa(xv[j], xv[j]), c[j]));
+                    float dn = dold;
+                    if (i == 0 || dn > d) {
+                        dn = d;
+                        d0[n] = d;
+                        idv[n] = i;
                     }
-                    if (cnt > 0 && lane == 0) ckpt[((base + k * 64) >> 6)] = run;
+                    sh.ring[b & 1][dt] = dn;
                 }
-            }
-            if (live) {
-                float d = fa(fa(cn, xn), 0.0f);
+                const int n2 = n + kYBlock;
+                if (b + 1 < nblk && n2 < N) {
 #pragma unroll
-                for (int j = 0; j < D; ++j) d = fs(d, fm(fa(xv[j], xv[j]), c[j]));
-                float dn = dold;
-                if (i == 0 || dn > d) {
-                    dn = d;
-                    d0[n] = d;
-                    idv[n] = i;
+                    for (int j = 0; j < D; ++j) xv[j] = X[(int64_t)n2 * D + j];
+                    xn = norm[n2];
+                    dold = d0[n2];
                 }
-                sh.ring[b & 1][tid] = dn;
+                __syncthreads();
             }
-            __syncthreads();
         }
-        if (wave == 0) total = run;
     }
     // ---- means of the seeding assignment (@0x180002290): c = f32(sum in point order) / f32(count)
     int* counts = i_scratch + fr.k_off;
