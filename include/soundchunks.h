@@ -97,6 +97,12 @@ int gsc_encode_wav_frames(const uint8_t *wav, size_t wav_len, const gsc_options 
                           uint8_t **out, size_t *out_len, int *frame_count);
 int gsc_count_frames(const uint8_t *wav, size_t wav_len, const gsc_options *o, int *frame_count);
 
+/* Device DSP of one frame (FindAttenuationDivider, encoder.lpr:566-605, and the
+ * MakeChunks features, encoder.lpr:467-485): *feat = n_chunks x 2*ChunkSize
+ * floats, allocated by the library (gsc_free).  Parity tests. */
+int gsc_frame_dsp(const uint8_t *wav, size_t wav_len, const gsc_options *o, int frame, int *atten_div, float **feat,
+                  int *n_chunks);
+
 /* Stage entry points on host buffers (row-major), used by parity tests. */
 int gsc_yakmo_seed_means(int n, int d, const float *x, int k, float *centroids);
 int gsc_scan_reduce(int n, int d, const float *x, int k, float *centroids, int *clusters, int precision, int *iters);
@@ -112,6 +118,7 @@ typedef struct {
     long long knnfit_pairs;      /* sum over frames of N * 4R (query x candidate) */
     int scan_launches, knnfit_launches;
     long long scan_restarts;     /* batched KNNScanReduce pipeline restarts */
+    double gpu_dsp_ms;           /* device DSP incl. sample upload (attenuation divider, features) */
 } gsc_timing;
 void gsc_last_timing(gsc_timing *t);
 

@@ -53,6 +53,7 @@ class GscTiming(ctypes.Structure):
         ("scan_launches", ctypes.c_int),
         ("knnfit_launches", ctypes.c_int),
         ("scan_restarts", ctypes.c_longlong),
+        ("gpu_dsp_ms", ctypes.c_double),
     ]
 
 
@@ -83,6 +84,8 @@ SIGNATURES = {
                                              ctypes.c_int, ctypes.POINTER(_U8P), ctypes.POINTER(ctypes.c_size_t),
                                              _IP]),
     "gsc_count_frames": (ctypes.c_int, [_U8P, ctypes.c_size_t, ctypes.POINTER(GscOptions), _IP]),
+    "gsc_frame_dsp": (ctypes.c_int, [_U8P, ctypes.c_size_t, ctypes.POINTER(GscOptions), ctypes.c_int, _IP,
+                                     ctypes.POINTER(_FP), _IP]),
     "gsc_yakmo_seed_means": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _FP, ctypes.c_int, _FP]),
     "gsc_scan_reduce": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _FP, ctypes.c_int, _FP, _IP, ctypes.c_int, _IP]),
     "gsc_knnfit_assign": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _FP, ctypes.c_int, _FP, ctypes.c_float, _IP]),

@@ -34,6 +34,18 @@ struct ReduceFrame {
     uint64_t stamps[96];  // out (GSC_STAMPS builds only): per-phase cycles, 12 per wave
 };
 
+// One frame of the encoder's per-frame DSP: FindAttenuationDivider
+// (encoder.lpr:566-605) and the MakeChunks features (encoder.lpr:467-485).
+struct DspFrame {
+    int64_t s_off;        // first sample of the frame in each channel row of the sample slab
+    int64_t x_off;        // features out: n*2CS floats at X + x_off (chunk-major, channel-minor)
+    int64_t c_off;        // per-chunk bytes out (neg | rev << 1) at +c_off
+    int32_t sc;           // frame sample count
+    int32_t n;            // chunks (chunk_count * channels)
+    int32_t atten_div;    // out: FindAttenuationDivider
+    int32_t pad_;
+};
+
 // One frame of TFrame.KNNFit (encoder.lpr:915-978).
 struct FitFrame {
     int64_t cand_off;     // R*CS floats: forward candidate values (neg/rev derived)

@@ -1,0 +1,226 @@
+// Per-frame DSP of the encoder on the device: FindAttenuationDivider
+// (encoder.lpr:566-605) and the chunk features of MakeChunks / TChunk
+// ComputeDCT (encoder.lpr:258-322, 349-363, 467-485, 1700-1716).  f64
+// throughout, in the reference's operation order (-ffp-contract=off, IEEE
+// division and sqrt), so the results equal the host restatement in
+// gsc_encoder.cpp bit for bit.
+//
+// Samples: one f64 row per channel (s / 32767, TEncoder.Load), row stride
+// `span`.  Features land in the slab yakmo / KNNScanReduce read (X), so they
+// never cross PCIe.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fpc_math.h"
+#include "gsc_device.h"
+
+namespace gsc {
+namespace {
+
+constexpr int kMaxAtt = 15;  // CMaxAttenuation (encoder.lpr:14)
+
+__device__ __forceinline__ int64_t ceil_pos_d(double x) {  // FPC math.ceil, x >= 0
+    const double t = trunc(x);
+    int64_t r = (int64_t)t;
+    if (x - t > 0.0) ++r;
+    return r;
+}
+
+// FindAttenuationDivider: lane = candidate law 1/(lane+1); each lane runs the
+// reference's sequential f64 error sum over (channel, chunk, sample), then the
+// first lane at the minimum wins (strict <, laws in order).
+template <int CS>
+__global__ __launch_bounds__(64) void atten_kernel(DspFrame* __restrict__ frames, int nframes,
+                                                   const double* __restrict__ samp, int64_t span, int ch, int obd) {
+    const int fi = blockIdx.x;
+    if (fi >= nframes) return;
+    DspFrame* fr = frames + fi;
+    const int lane = threadIdx.x;
+    const double law = 1.0 / double(lane + 1);
+    // coeff(a) = 1 + sum_{i=0..a} i*law, left to right (encoder.lpr:1654-1656)
+    double coeff[kMaxAtt + 1];
+    {
+        double c = 1.0;
+#pragma unroll
+        for (int a = 0; a <= kMaxAtt; ++a) {
+            c += double(a) * law;
+            coeff[a] = c;
+        }
+    }
+    const int sc = fr->sc, nck = sc / CS;
+    const double dobd = double(obd);
+    double v = 0.0;
+    for (int j = 0; j < ch; ++j) {
+        const double* src = samp + int64_t(j) * span + fr->s_off;
+        for (int k = 0; k < nck; ++k) {
+            double x[CS];
+#pragma unroll
+            for (int l = 0; l < CS; ++l) x[l] = src[k * CS + l];
+            // hiSmp (encoder.lpr:1687-1689)
+            int64_t hi = 0;
+#pragma unroll
+            for (int l = 0; l < CS; ++l) {
+                const int64_t h = ceil_pos_d(fabs(x[l] * 32767.0));
+                hi = h > hi ? h : hi;
+            }
+            // ComputeAttenuation (encoder.lpr:1691-1697): coeff after r steps = coeff[r]
+            int a = kMaxAtt;
+            for (int r = 1; r <= kMaxAtt; ++r)
+                if (double(hi) * coeff[r] > 32767.0) {
+                    a = r - 1;
+                    break;
+                }
+            double cf = coeff[0];
+#pragma unroll
+            for (int q = 1; q <= kMaxAtt; ++q) cf = q == a ? coeff[q] : cf;
+            const double den = dobd * cf;
+#pragma unroll
+            for (int l = 0; l < CS; ++l) {
+                // makeOutputSample (encoder.lpr:1648-1663): Round, SmallInt wrap, clamp
+                int s16 = (int)(int16_t)(int64_t)rint(x[l] * dobd * cf);
+                s16 = max(s16, -obd + 1);
+                s16 = min(s16, obd - 1);
+                // makeFloatSample (encoder.lpr:1665-1680)
+                double r = double(s16) / den;
+                r = r < -1.0 ? -1.0 : r;
+                r = r > 1.0 ? 1.0 : r;
+                const double dd = x[l] - r;
+                v += dd * dd;
+            }
+        }
+    }
+    // first lane at the minimum (best starts at MaxSingle, v < best)
+    double best = v;
+    int bi = lane;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double ov = __shfl_xor(best, o);
+        const int oi = __shfl_xor(bi, o);
+        if (ov < best || (ov == best && oi < bi)) {
+            best = ov;
+            bi = oi;
+        }
+    }
+    if (lane == 0) fr->atten_div = best < 3.4028234663852886e+38 ? bi + 1 : 1;
+}
+
+struct Trig {
+    double dct[16 * 16], dft_c[16 * 16], dft_s[16 * 16], idft_c[16 * 16], idft_s[16 * 16];
+};
+
+// one chunk per thread: srcData, sign / reverse heuristics, DCT-II, cepstrum
+template <int CS>
+__global__ __launch_bounds__(256) void features_kernel(const DspFrame* __restrict__ frames, int nframes,
+                                                       const double* __restrict__ samp, int64_t span, int ch,
+                                                       const double* __restrict__ trig_g, double s0, double scale,
+                                                       float* __restrict__ X, uint8_t* __restrict__ nr) {
+    __shared__ double tr[5 * CS * CS];
+    for (int i = threadIdx.x; i < 5 * CS * CS; i += blockDim.x) tr[i] = trig_g[i];
+    __syncthreads();
+    const double* dct = tr;
+    const double* dft_c = tr + CS * CS;
+    const double* dft_s = tr + 2 * CS * CS;
+    const double* idft_c = tr + 3 * CS * CS;
+    const double* idft_s = tr + 4 * CS * CS;
+    const int fi = blockIdx.y;
+    if (fi >= nframes) return;
+    const DspFrame fr = frames[fi];
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= fr.n) return;
+    const int i = c / ch, j = c - i * ch;
+    // chunk samples, zero past the frame end (encoder.lpr:467-485: 0 + sample)
+    double s[CS];
+    const double* row = samp + int64_t(j) * span + fr.s_off;
+#pragma unroll
+    for (int k = 0; k < CS; ++k) {
+        const int pos = i * CS + k;
+        s[k] = pos >= fr.sc ? 0.0 : 0.0 + row[pos];
+    }
+    // TChunk.ComputeDstAttributes sign / reverse (encoder.lpr:374-396)
+    double p1 = 0.0, p2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < CS; ++k)
+        if (s[k] < 0) p1 -= s[k];
+#pragma unroll
+    for (int k = 0; k < CS; ++k)
+        if (s[k] > 0) p2 += s[k];
+    const bool neg = p1 > p2;
+    p1 = 0.0;
+    p2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < CS / 2; ++k) p1 += fabs(s[k]);
+#pragma unroll
+    for (int k = CS / 2; k < CS; ++k) p2 += fabs(s[k]);
+    const bool rev = p1 > p2;
+    nr[fr.c_off + c] = (uint8_t)((neg ? 1 : 0) | (rev ? 2 : 0));
+    double data[CS], temp[CS];
+#pragma unroll
+    for (int k = 0; k < CS; ++k) data[k] = s[rev ? CS - 1 - k : k] * (neg ? -1.0 : 1.0);
+    float* out = X + fr.x_off + int64_t(c) * 2 * CS;
+    // DCT-II (encoder.lpr:258-276)
+#pragma unroll
+    for (int k = 0; k < CS; ++k) {
+        const double sk = k == 0 ? s0 : 1.0;
+        double sum = 0.0;
+#pragma unroll
+        for (int n = 0; n < CS; ++n) sum += sk * data[n] * dct[k * CS + n];
+        out[k] = float(sum * scale);
+    }
+    // power spectrum, log10, inverse DFT magnitude * 1e-5 (encoder.lpr:278-322, 1700-1716)
+#pragma unroll
+    for (int k = 0; k < CS; ++k) {
+        double re = 0.0, im = 0.0;
+#pragma unroll
+        for (int q = 0; q < CS; ++q) {
+            re += data[q] * dft_c[k * CS + q];
+            im += data[q] * dft_s[k * CS + q];
+        }
+        temp[k] = re * re + im * im;
+    }
+#pragma unroll
+    for (int k = 0; k < CS; ++k)
+        if (!fpc::is_zero(temp[k])) temp[k] = fpc::log10(temp[k]);
+#pragma unroll
+    for (int k = 0; k < CS; ++k) {
+        double re = 0.0, im = 0.0;
+#pragma unroll
+        for (int q = 0; q < CS; ++q) {
+            re += temp[q] * idft_c[k * CS + q];
+            im += temp[q] * idft_s[k * CS + q];
+        }
+        re /= double(CS);
+        im /= double(CS);
+        out[CS + k] = float(__dsqrt_rn(re * re + im * im) * 0.00001);
+    }
+}
+
+}  // namespace
+}  // namespace gsc
+
+using namespace gsc;
+
+// FindAttenuationDivider for every frame (one wave per frame)
+extern "C" hipError_t gsc_launch_atten(int cs, DspFrame* frames, int nframes, const double* samp, int64_t span, int ch,
+                                       int obd, hipStream_t st) {
+    switch (cs) {
+    case 4: hipLaunchKernelGGL(atten_kernel<4>, dim3(nframes), dim3(64), 0, st, frames, nframes, samp, span, ch, obd); break;
+    case 8: hipLaunchKernelGGL(atten_kernel<8>, dim3(nframes), dim3(64), 0, st, frames, nframes, samp, span, ch, obd); break;
+    case 16: hipLaunchKernelGGL(atten_kernel<16>, dim3(nframes), dim3(64), 0, st, frames, nframes, samp, span, ch, obd); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// chunk features for every frame; trig = 5 CS x CS f64 tables (dct, dft cos/sin, idft cos/sin)
+extern "C" hipError_t gsc_launch_features(int cs, const DspFrame* frames, int nframes, int max_n, const double* samp,
+                                          int64_t span, int ch, const double* trig, double s0, double scale, float* X,
+                                          uint8_t* nr, hipStream_t st) {
+    const dim3 grid((max_n + 255) / 256, nframes), block(256);
+    switch (cs) {
+    case 4: hipLaunchKernelGGL(features_kernel<4>, grid, block, 0, st, frames, nframes, samp, span, ch, trig, s0, scale, X, nr); break;
+    case 8: hipLaunchKernelGGL(features_kernel<8>, grid, block, 0, st, frames, nframes, samp, span, ch, trig, s0, scale, X, nr); break;
+    case 16: hipLaunchKernelGGL(features_kernel<16>, grid, block, 0, st, frames, nframes, samp, span, ch, trig, s0, scale, X, nr); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}

@@ -106,45 +106,6 @@ const TrigTables& trig_for(int cs) {
     return t;
 }
 
-// TChunk.ComputeDCT: canonicalise, DCT-II, cepstrum*1e-5 (encoder.lpr:258-322,349-363,1700-1716)
-void chunk_features(const TrigTables& t, const double* src, bool neg, bool rev, float* out) {
-    const int cs = t.cs;
-    double data[16], temp[16];
-    for (int i = 0; i < cs; ++i) data[i] = src[rev ? cs - 1 - i : i] * (neg ? -1.0 : 1.0);
-    const double s0 = std::sqrt(0.5), scale = std::sqrt(2.0 / double(cs));
-    for (int k = 0; k < cs; ++k) {
-        const double s = k == 0 ? s0 : 1.0;
-        double sum = 0.0;
-        const double* cr = &t.dct[size_t(k) * cs];
-        for (int n = 0; n < cs; ++n) sum += s * data[n] * cr[n];
-        out[k] = float(sum * scale);
-    }
-    for (int k = 0; k < cs; ++k) {
-        double re = 0.0, im = 0.0;
-        const double* cr = &t.dft_c[size_t(k) * cs];
-        const double* sr = &t.dft_s[size_t(k) * cs];
-        for (int i = 0; i < cs; ++i) {
-            re += data[i] * cr[i];
-            im += data[i] * sr[i];
-        }
-        temp[k] = re * re + im * im;
-    }
-    for (int i = 0; i < cs; ++i)
-        if (!fpc::is_zero(temp[i])) temp[i] = fpc::log10(temp[i]);
-    for (int k = 0; k < cs; ++k) {
-        double re = 0.0, im = 0.0;
-        const double* cr = &t.idft_c[size_t(k) * cs];
-        const double* sr = &t.idft_s[size_t(k) * cs];
-        for (int i = 0; i < cs; ++i) {
-            re += temp[i] * cr[i];
-            im += temp[i] * sr[i];
-        }
-        re /= double(cs);
-        im /= double(cs);
-        out[cs + k] = float(std::sqrt(re * re + im * im) * 0.00001);
-    }
-}
-
 // FPC TFPSList.QuickSort (encoder.exe @0x10003d410) on `items`, count descending
 void fpc_quicksort(int* items, const int* count, int L, int R) {
     int I, J, P;
@@ -178,6 +139,14 @@ inline int bsr_word(unsigned v) {
 }  // namespace
 
 void warm_trig_tables(int cs) { (void)trig_for(cs); }
+
+void trig_pack(int cs, std::vector<double>* tab, double* s0, double* scale) {
+    const TrigTables& t = trig_for(cs);
+    tab->clear();
+    for (const auto* v : {&t.dct, &t.dft_c, &t.dft_s, &t.idft_c, &t.idft_s}) tab->insert(tab->end(), v->begin(), v->end());
+    *s0 = std::sqrt(0.5);
+    *scale = std::sqrt(2.0 / double(cs));
+}
 
 // TEncoder.Load + PrepareFrames (encoder.lpr:1111-1152, 1241-1273, 1294-1429)
 int Encoder::prepare(const uint8_t* wav, size_t len, std::string* err) {
@@ -280,68 +249,24 @@ int Encoder::prepare(const uint8_t* wav, size_t len, std::string* err) {
     return 0;
 }
 
-// FindAttenuationDivider (encoder.lpr:566-605) + MakeChunks features (467-485, 349-363)
-void Encoder::frame_host_prepare(FrameState& f) const {
-    const int cs = opt_.chunk_size, ch = channels_, bd = opt_.chunk_bit_depth;
+// MakeChunks srcData (encoder.lpr:467-485): chunk-major, channel-minor, zero
+// past the frame end.  FindAttenuationDivider, the sign / reverse flags and
+// the features run on the device (gsc_dsp.hip).
+void Encoder::frame_host_src(FrameState& f) const {
+    const int cs = opt_.chunk_size, ch = channels_;
     const int sc = f.sample_count;
-    const int obd = (1 << (bd - 1)) - 1;
-    // --- attenuation divider: hiSmp per chunk is law-independent ---
-    const int nck = sc / cs;
-    std::vector<int64_t> hi(size_t(ch) * std::max(nck, 1));
-    for (int j = 0; j < ch; ++j)
-        for (int k = 0; k < nck; ++k) hi[size_t(j) * nck + k] = hi_sample(&filtered_[j][f.start + k * cs], cs);
-    int best_div = 1;
-    double best = 3.4028234663852886e+38;  // MaxSingle
-    std::vector<double> fs_tab(size_t(16) * (2 * obd + 1));
-    double coeff[16];
-    for (int i = 1; i <= 64; ++i) {
-        const double law = 1.0 / double(i);
-        for (int a = 0; a < 16; ++a) {
-            coeff[a] = atten_coeff(a, law);
-            for (int s = -obd; s <= obd; ++s)
-                fs_tab[size_t(a) * (2 * obd + 1) + (s + obd)] = float_sample(int16_t(s), double(obd), coeff[a], false);
-        }
-        double v = 0.0;
-        for (int j = 0; j < ch; ++j) {
-            const double* src = &filtered_[j][f.start];
-            for (int k = 0; k < nck; ++k) {
-                const int a = attenuation_of(hi[size_t(j) * nck + k], law);
-                const double* tab = &fs_tab[size_t(a) * (2 * obd + 1) + obd];
-                for (int l = 0; l < cs; ++l) {
-                    const double x = src[k * cs + l];
-                    const int16_t os = output_sample(x, obd, coeff[a], false);
-                    const double dd = x - tab[os];
-                    v += dd * dd;
-                }
-            }
-        }
-        if (v < best) {
-            best = v;
-            best_div = i;
-        }
-    }
-    f.atten_div = best_div;
-    // --- chunks: srcData, sign/reverse, features ---
     const int chunk_count = (sc - 1) / cs + 1;
     f.n = chunk_count * ch;
     f.src.assign(size_t(f.n) * cs, 0.0);
-    f.feat.assign(size_t(f.n) * 2 * cs, 0.0f);
     f.neg.assign(size_t(f.n), 0);
     f.rev.assign(size_t(f.n), 0);
-    const TrigTables& t = trig_for(cs);
     for (int i = 0; i < chunk_count; ++i)
         for (int j = 0; j < ch; ++j) {
-            const int c = i * ch + j;
-            double* s = &f.src[size_t(c) * cs];
+            double* s = &f.src[size_t(i * ch + j) * cs];
             for (int k = 0; k < cs; ++k) {
                 const int pos = i * cs + k;
                 s[k] = pos >= sc ? 0.0 : 0.0 + filtered_[j][f.start + pos];
             }
-            bool ng, rv;
-            sign_reverse(s, cs, &ng, &rv);
-            f.neg[c] = ng;
-            f.rev[c] = rv;
-            chunk_features(t, s, ng, rv, &f.feat[size_t(c) * 2 * cs]);
         }
 }
 

@@ -20,7 +20,6 @@ struct FrameState {
     int atten_div = 6;
     int n = 0;                 // chunkRefs count (chunk-major, channel-minor)
     std::vector<double> src;   // n*CS srcData
-    std::vector<float> feat;   // n*2CS Single(dct)
     std::vector<uint8_t> neg, rev;
     std::vector<int> red;      // final reduced-chunk index per chunk
     // reduced chunks
@@ -41,6 +40,9 @@ struct FrameState {
 // Builds the exact FPC trig tables for chunk size cs (not thread-safe: call
 // before starting per-frame workers).
 void warm_trig_tables(int cs);
+// The same tables packed for the device DSP: dct, dft cos, dft sin, idft cos,
+// idft sin (cs*cs f64 each), plus the DCT scale factors sqrt(1/2), sqrt(2/cs).
+void trig_pack(int cs, std::vector<double>* tab, double* s0, double* scale);
 
 class Encoder {
    public:
@@ -50,13 +52,20 @@ class Encoder {
     int frame_count() const { return int(fr_start_.size()); }
     // Encode frames [b, e) and return their concatenated stream bytes
     int encode_range(int b, int e, std::vector<uint8_t>* out, std::string* err, gsc_timing* tim);
+    // Device DSP of frame f alone (parity tests): attenuation divider and the
+    // N x 2CS features
+    int dsp_frame(int f, int* atten_div, std::vector<float>* feat, std::string* err);
 
     int channels() const { return channels_; }
     int sample_rate() const { return sample_rate_; }
     long long sample_count() const { return sample_count_; }
 
    private:
-    void frame_host_prepare(FrameState& f) const;
+    void frame_host_src(FrameState& f) const;  // chunk count + srcData (encoder.lpr:467-485)
+    // device DSP for frames (first frame index b): atten_div, neg / rev on the
+    // host side, features left in the device slab *dX at (*xoff)[i]
+    int device_dsp(int b, std::vector<FrameState>& frames, void* dX, std::vector<int64_t>* xoff, double* ms,
+                   std::string* err);
     void frame_reduce_post(FrameState& f, bool reduced) const;
     void frame_knnfit_post(FrameState& f) const;
     void frame_save(FrameState& f) const;

@@ -30,6 +30,11 @@ extern "C" hipError_t gsc_launch_scan_pass(int D, gsc::ReduceFrame* frames, int 
 extern "C" hipError_t gsc_launch_scan_batch(int D, int logk, gsc::ReduceFrame* frames, int nframes, const float* X,
                                             float* C, int* is, const float* rate_tab, double tol, int pass,
                                             hipStream_t st);
+extern "C" hipError_t gsc_launch_atten(int cs, gsc::DspFrame* frames, int nframes, const double* samp, int64_t span,
+                                       int ch, int obd, hipStream_t st);
+extern "C" hipError_t gsc_launch_features(int cs, const gsc::DspFrame* frames, int nframes, int max_n,
+                                          const double* samp, int64_t span, int ch, const double* trig, double s0,
+                                          double scale, float* X, uint8_t* nr, hipStream_t st);
 extern "C" hipError_t gsc_launch_knnfit(int CS, gsc::FitFrame* frames, int nframes, int max_n, int max_r,
                                         const float* cand, const float* q, int* out, hipStream_t st);
 
@@ -180,9 +185,10 @@ std::vector<float> rate_table(int n) {
 
 // Reduce (yakmo seeding + KNNScanReduce) for a batch of frames; X/C host arrays
 // are concatenated per frame (N_f*D and K*D floats).
-int run_reduce_batch(int D, int K, int precision, const std::vector<int>& Ns, const std::vector<float>& X,
-                     std::vector<float>* C, std::vector<int>* clusters, std::vector<int>* iters, std::vector<int>* slow,
-                     long long* restarts, double* yakmo_ms, double* scan_ms) {
+// X: device slab, frame i's N_i x D features at dX + xoff[i]
+int run_reduce_batch_dev(int D, int K, int precision, const std::vector<int>& Ns, const std::vector<int64_t>& xoff,
+                         const float* dX, std::vector<float>* C, std::vector<int>* clusters, std::vector<int>* iters,
+                         std::vector<int>* slow, long long* restarts, double* yakmo_ms, double* scan_ms) {
     // launches: one yakmo launch + kMaxScanIters scan launches per batch
     const int nf = int(Ns.size());
     if (nf == 0) return 0;
@@ -190,16 +196,15 @@ int run_reduce_batch(int D, int K, int precision, const std::vector<int>& Ns, co
     for (int n : Ns)
         if (n > 262144) return fail("frame has more than 262144 chunks (yakmo seeding bitmap)");
     std::vector<ReduceFrame> fr(static_cast<size_t>(nf));
-    int64_t xo = 0, no = 0, maxN = 0;
+    int64_t no = 0, maxN = 0;
     for (int i = 0; i < nf; ++i) {
         fr[i] = ReduceFrame{};
-        fr[i].x_off = xo;
+        fr[i].x_off = xoff[i];
         fr[i].c_off = int64_t(i) * K * D;
         fr[i].n_off = no;
         fr[i].k_off = 0;  // filled below
         fr[i].N = Ns[i];
         fr[i].K = K;
-        xo += int64_t(Ns[i]) * D;
         no += Ns[i];
         maxN = std::max<int64_t>(maxN, Ns[i]);
     }
@@ -207,11 +212,10 @@ int run_reduce_batch(int D, int K, int precision, const std::vector<int>& Ns, co
         fr[i].k_off = no + int64_t(i) * K;
         fr[i].ka_off = no + int64_t(nf + i) * K;
     }
-    DevBuf<float> dX, dC, dF, dRate;
+    DevBuf<float> dC, dF, dRate;
     DevBuf<int> dI;
     DevBuf<uint32_t> dBits;
     DevBuf<ReduceFrame> dFr;
-    HIP_TRY(dX.alloc(size_t(xo)));
     HIP_TRY(dC.alloc(size_t(nf) * K * D));
     HIP_TRY(dF.alloc(size_t(no) * 4));
     HIP_TRY(dI.alloc(size_t(no) + 2 * size_t(nf) * K));
@@ -219,7 +223,6 @@ int run_reduce_batch(int D, int K, int precision, const std::vector<int>& Ns, co
     HIP_TRY(dFr.alloc(size_t(nf)));
     const std::vector<float> rt = rate_table(int(maxN));
     HIP_TRY(dRate.alloc(rt.size()));
-    HIP_TRY(hipMemcpy(dX.p, X.data(), sizeof(float) * size_t(xo), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(dRate.p, rt.data(), sizeof(float) * rt.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(dFr.p, fr.data(), sizeof(ReduceFrame) * size_t(nf), hipMemcpyHostToDevice));
     hipEvent_t e0, e1, e2;
@@ -227,9 +230,9 @@ int run_reduce_batch(int D, int K, int precision, const std::vector<int>& Ns, co
     HIP_TRY(hipEventCreate(&e1));
     HIP_TRY(hipEventCreate(&e2));
     HIP_TRY(hipEventRecord(e0, nullptr));
-    HIP_TRY(gsc_launch_yakmo(D, dFr.p, nf, dX.p, dC.p, dF.p, dI.p, dBits.p, nullptr));
+    HIP_TRY(gsc_launch_yakmo(D, dFr.p, nf, dX, dC.p, dF.p, dI.p, dBits.p, nullptr));
     HIP_TRY(hipEventRecord(e1, nullptr));
-    HIP_TRY(launch_scan_passes(D, dFr.p, nf, K, dX.p, dC.p, dI.p, dF.p, dRate.p, precision));
+    HIP_TRY(launch_scan_passes(D, dFr.p, nf, K, dX, dC.p, dI.p, dF.p, dRate.p, precision));
     HIP_TRY(hipEventRecord(e2, nullptr));
     HIP_TRY(hipEventSynchronize(e2));
     float t1 = 0, t2 = 0;
@@ -254,6 +257,23 @@ int run_reduce_batch(int D, int K, int precision, const std::vector<int>& Ns, co
         if (fr[i].loop_iters < 0) return fail("KNNScanReduce: batched pipeline made no progress (guard tripped)");
     }
     return 0;
+}
+
+// host X: frames concatenated (N_f * D floats each)
+int run_reduce_batch(int D, int K, int precision, const std::vector<int>& Ns, const std::vector<float>& X,
+                     std::vector<float>* C, std::vector<int>* clusters, std::vector<int>* iters, std::vector<int>* slow,
+                     long long* restarts, double* yakmo_ms, double* scan_ms) {
+    std::vector<int64_t> xoff(Ns.size());
+    int64_t xo = 0;
+    for (size_t i = 0; i < Ns.size(); ++i) {
+        xoff[i] = xo;
+        xo += int64_t(Ns[i]) * D;
+    }
+    DevBuf<float> dX;
+    HIP_TRY(dX.alloc(size_t(xo)));
+    HIP_TRY(hipMemcpy(dX.p, X.data(), sizeof(float) * size_t(xo), hipMemcpyHostToDevice));
+    return run_reduce_batch_dev(D, K, precision, Ns, xoff, dX.p, C, clusters, iters, slow, restarts, yakmo_ms,
+                                scan_ms);
 }
 
 int run_knnfit_batch(int CS, const std::vector<int>& Rs, const std::vector<int>& Ns, const std::vector<float>& eps,
@@ -311,7 +331,105 @@ int run_knnfit_batch(int CS, const std::vector<int>& Rs, const std::vector<int>&
 
 }  // namespace
 
-// ---- Encoder::encode_range: host DSP || device hot path -------------------
+// ---- Encoder::device_dsp: FindAttenuationDivider + features on the device --
+// dXv: DevBuf<float>* that receives the feature slab (kept for the Reduce).
+int Encoder::device_dsp(int b, std::vector<FrameState>& frames, void* dXv, std::vector<int64_t>* xoff, double* ms,
+                        std::string* err) {
+    auto& dX = *static_cast<DevBuf<float>*>(dXv);
+    const int cs = opt_.chunk_size, ch = channels_, nfr = int(frames.size());
+    const int obd = (1 << (opt_.chunk_bit_depth - 1)) - 1;
+    const int e = b + nfr;
+    const int64_t s_first = fr_start_[b], span = int64_t(fr_end_[e - 1]) - s_first + 1;
+    std::vector<DspFrame> df(static_cast<size_t>(nfr));
+    xoff->assign(size_t(nfr), 0);
+    int64_t xo = 0, co = 0;
+    int max_n = 0;
+    for (int i = 0; i < nfr; ++i) {
+        const FrameState& f = frames[i];
+        df[i] = DspFrame{};
+        df[i].s_off = int64_t(f.start) - s_first;
+        df[i].x_off = xo;
+        df[i].c_off = co;
+        df[i].sc = f.sample_count;
+        df[i].n = f.n;
+        (*xoff)[i] = xo;
+        xo += int64_t(f.n) * 2 * cs;
+        co += f.n;
+        max_n = std::max(max_n, f.n);
+    }
+    std::vector<double> trig;
+    double s0 = 0, scale = 0;
+    trig_pack(cs, &trig, &s0, &scale);
+    DevBuf<double> dS, dT;
+    DevBuf<DspFrame> dF;
+    DevBuf<uint8_t> dNR;
+    const double t0 = now_ms();
+    if (dS.alloc(size_t(ch) * size_t(span)) != hipSuccess || dT.alloc(trig.size()) != hipSuccess ||
+        dF.alloc(size_t(nfr)) != hipSuccess || dNR.alloc(size_t(co)) != hipSuccess || dX.alloc(size_t(xo)) != hipSuccess) {
+        *err = "device DSP: out of device memory";
+        return -1;
+    }
+    auto chk = [&](hipError_t r, const char* what) {
+        if (r == hipSuccess) return true;
+        *err = std::string("device DSP: ") + what + ": " + hipGetErrorString(r);
+        return false;
+    };
+    for (int j = 0; j < ch; ++j)
+        if (!chk(hipMemcpy(dS.p + size_t(j) * size_t(span), filtered_[j].data() + s_first, sizeof(double) * size_t(span),
+                           hipMemcpyHostToDevice),
+                 "sample upload"))
+            return -1;
+    if (!chk(hipMemcpy(dT.p, trig.data(), sizeof(double) * trig.size(), hipMemcpyHostToDevice), "trig upload") ||
+        !chk(hipMemcpy(dF.p, df.data(), sizeof(DspFrame) * size_t(nfr), hipMemcpyHostToDevice), "frame upload") ||
+        !chk(gsc_launch_atten(cs, dF.p, nfr, dS.p, span, ch, obd, nullptr), "atten launch") ||
+        !chk(gsc_launch_features(cs, dF.p, nfr, max_n, dS.p, span, ch, dT.p, s0, scale, dX.p, dNR.p, nullptr),
+             "features launch"))
+        return -1;
+    std::vector<uint8_t> nr(static_cast<size_t>(co));
+    if (!chk(hipMemcpy(df.data(), dF.p, sizeof(DspFrame) * size_t(nfr), hipMemcpyDeviceToHost), "frame download") ||
+        !chk(hipMemcpy(nr.data(), dNR.p, size_t(co), hipMemcpyDeviceToHost), "flag download"))
+        return -1;
+    for (int i = 0; i < nfr; ++i) {
+        FrameState& f = frames[i];
+        f.atten_div = df[i].atten_div;
+        const uint8_t* q = nr.data() + df[i].c_off;
+        for (int c = 0; c < f.n; ++c) {
+            f.neg[c] = q[c] & 1;
+            f.rev[c] = (q[c] >> 1) & 1;
+        }
+    }
+    if (ms) *ms += now_ms() - t0;
+    return 0;
+}
+
+int Encoder::dsp_frame(int fi, int* atten_div, std::vector<float>* feat, std::string* err) {
+    if (ensure_device() != 0) {
+        *err = t_err;
+        return -1;
+    }
+    if (fi < 0 || fi >= frame_count()) {
+        *err = "frame index out of range";
+        return -1;
+    }
+    warm_trig_tables(opt_.chunk_size);
+    std::vector<FrameState> frames(1);
+    frames[0].index = fi;
+    frames[0].start = fr_start_[fi];
+    frames[0].sample_count = fr_end_[fi] - fr_start_[fi] + 1;
+    frame_host_src(frames[0]);
+    DevBuf<float> dX;
+    std::vector<int64_t> xoff;
+    if (device_dsp(fi, frames, &dX, &xoff, nullptr, err) != 0) return -1;
+    *atten_div = frames[0].atten_div;
+    feat->resize(size_t(frames[0].n) * 2 * opt_.chunk_size);
+    if (hipMemcpy(feat->data(), dX.p, sizeof(float) * feat->size(), hipMemcpyDeviceToHost) != hipSuccess) {
+        *err = "feature download failed";
+        return -1;
+    }
+    return 0;
+}
+
+// ---- Encoder::encode_range: host srcData, device DSP + hot path ------------
 int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* err, gsc_timing* tim) {
     if (ensure_device() != 0) {
         *err = t_err;
@@ -327,27 +445,29 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
         f.index = b + i;
         f.start = fr_start_[b + i];
         f.sample_count = fr_end_[b + i] - fr_start_[b + i] + 1;
-        frame_host_prepare(f);
+        frame_host_src(f);
     });
+    double dsp_ms = 0;
+    DevBuf<float> dFeat;
+    std::vector<int64_t> feat_off;
+    if (nfr > 0 && device_dsp(b, frames, &dFeat, &feat_off, &dsp_ms, err) != 0) return -1;
     double t1 = now_ms();
     // --- Reduce on the device for frames with more chunks than ChunksPerFrame
     std::vector<int> red_idx, Ns;
+    std::vector<int64_t> red_xoff;
     for (int i = 0; i < nfr; ++i)
         if (opt_.precision > 0 && frames[i].n > K) {
             red_idx.push_back(i);
             Ns.push_back(frames[i].n);
+            red_xoff.push_back(feat_off[i]);
         }
     double yak_ms = 0, scan_ms = 0, knn_ms = 0;
     long long passes = 0, slow = 0, restarts = 0;
     if (!red_idx.empty()) {
-        std::vector<float> X;
-        size_t tot = 0;
-        for (int i : red_idx) tot += frames[i].feat.size();
-        X.reserve(tot);
-        for (int i : red_idx) X.insert(X.end(), frames[i].feat.begin(), frames[i].feat.end());
         std::vector<float> C;
         std::vector<int> cl, it, sl;
-        if (run_reduce_batch(D, K, opt_.precision, Ns, X, &C, &cl, &it, &sl, &restarts, &yak_ms, &scan_ms) != 0) {
+        if (run_reduce_batch_dev(D, K, opt_.precision, Ns, red_xoff, dFeat.p, &C, &cl, &it, &sl, &restarts, &yak_ms,
+                                 &scan_ms) != 0) {
             *err = t_err;
             return -1;
         }
@@ -415,7 +535,8 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
     for (auto& f : frames) out->insert(out->end(), f.stream.begin(), f.stream.end());
     double t4 = now_ms();
     if (tim) {
-        tim->host_frames_ms = t1 - t0;
+        tim->host_frames_ms = t1 - t0 - dsp_ms;
+        tim->gpu_dsp_ms = dsp_ms;
         tim->gpu_yakmo_ms = yak_ms;
         tim->gpu_scan_ms = scan_ms;
         tim->gpu_knnfit_ms = knn_ms;
@@ -531,6 +652,19 @@ int gsc_encode_wav_frames(const uint8_t* wav, size_t wav_len, const gsc_options*
     *out_len = bytes.size();
     t_tim.host_prepare_ms = t1 - t0;
     t_tim.total_ms = now_ms() - t0;
+    return 0;
+}
+
+int gsc_frame_dsp(const uint8_t* wav, size_t wav_len, const gsc_options* o, int frame, int* atten_div, float** feat,
+                  int* n_chunks) {
+    Encoder enc(*o);
+    std::string err;
+    if (enc.prepare(wav, wav_len, &err) != 0) return fail(err);
+    std::vector<float> f;
+    if (enc.dsp_frame(frame, atten_div, &f, &err) != 0) return fail(err);
+    *n_chunks = int(f.size() / size_t(2 * o->chunk_size));
+    *feat = static_cast<float*>(std::malloc(std::max<size_t>(f.size(), 1) * sizeof(float)));
+    if (!f.empty()) std::memcpy(*feat, f.data(), f.size() * sizeof(float));
     return 0;
 }
 

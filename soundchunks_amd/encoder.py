@@ -114,3 +114,21 @@ def knnfit_assign(cand_fwd: np.ndarray, q: np.ndarray, eps: float) -> np.ndarray
     _lib.check(_lib.load().gsc_knnfit_assign(cand_fwd.shape[0], cand_fwd.shape[1], _fp(cand_fwd), q.shape[0],
                                              _fp(q), ctypes.c_float(eps), _ip(out)))
     return out
+
+
+def frame_dsp(wav: bytes, frame: int = 0, argv: Sequence[str] = ()) -> tuple[int, np.ndarray]:
+    """Device DSP of one frame: (attenuation divider, N x 2CS features)."""
+    o = parse_options(argv)
+    a, ptr = _u8(wav)
+    att = ctypes.c_int(0)
+    n = ctypes.c_int(0)
+    feat = ctypes.POINTER(ctypes.c_float)()
+    lib = _lib.load()
+    _lib.check(lib.gsc_frame_dsp(ptr, len(a), ctypes.byref(o), frame, ctypes.byref(att), ctypes.byref(feat),
+                                 ctypes.byref(n)))
+    try:
+        d = 2 * o.chunk_size
+        x = np.ctypeslib.as_array(feat, shape=(n.value * d,)).copy().reshape(n.value, d)
+    finally:
+        lib.gsc_free(ctypes.cast(feat, ctypes.c_void_p))
+    return att.value, x
