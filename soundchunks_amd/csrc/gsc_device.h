@@ -31,7 +31,7 @@ struct ReduceFrame {
     int32_t loop_iters;   // out: batched-pipeline iterations (diagnostic); -1 = guard tripped
     int32_t tree_exact;   // out: passes whose kd-tree needed the sequential build (median ties)
     int32_t pad_;
-    uint64_t stamps[96];  // out (GSC_STAMPS builds only): per-phase cycles, 12 per wave
+    uint64_t stamps[128]; // out (GSC_STAMPS builds only): per-phase cycles, 16 per wave
 };
 
 // One frame of the encoder's per-frame DSP: FindAttenuationDivider

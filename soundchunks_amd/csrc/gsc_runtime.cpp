@@ -744,10 +744,10 @@ int gsc_scan_reduce(int n, int d, const float* x, int k, float* centroids, int* 
     {
         std::fprintf(stderr, "scan: passes %d slow %d restarts %d loop_iters(last pass) %d err %.9g tree_exact %d\n",
                      fr[0].iters, fr[0].slow, fr[0].restarts, fr[0].loop_iters, fr[0].err, fr[0].tree_exact);
-        std::fprintf(stderr, "stamps [prep A1 vcheck B2 part3 part4 B1 vpend wonA2 setup soloA soloDFS]");
+        std::fprintf(stderr, "stamps [prep A1 A2 B2 part3 part4 B1 vcheck won setup soloA soloDFS a2win a2far a2box a2out]");
         for (int w = 0; w < 8; ++w) {
             std::fprintf(stderr, "\n  w%d:", w);
-            for (int k = 0; k < 12; ++k) std::fprintf(stderr, " %.3g", double(fr[0].stamps[w * 12 + k]));
+            for (int k = 0; k < 16; ++k) std::fprintf(stderr, " %.3g", double(fr[0].stamps[w * 16 + k]));
         }
         std::fprintf(stderr, "\n");
     }

@@ -51,6 +51,7 @@ namespace gsc {
 
 constexpr int kBatch = 32;         // queries per speculative batch (log window 2*kBatch <= 64)
 constexpr int kVer = 64 + kBatch;  // centroid versions seen by a pending batch
+constexpr int kRow = 20;           // coordinate row stride of lane-indexed LDS rows (80 B: no b128 bank conflicts)
 
 struct WaveRec {      // A1 output per (wave, query)
     uint32_t minbits; // wave minimum distance (f32 bits; distances are >= 0)
@@ -85,14 +86,14 @@ struct Scan2Shared {
     QRec qrec[2][kBatch];
     QRec qsolo;
     // update log: entry e = wave-0 lane e (position in a VGPR, coordinates here)
-    float lg_c[64][16];
+    float lg_c[64][kRow];
     int pub_pos[64];
-    float pub_c[64][16];
+    float pub_c[64][kRow];
     // commit of the pending batch: versions 0..63 = log entries, 64+j = after query j
     int vpos[kVer];
     int vfrom[kVer];   // first query that sees the version
     int vto[kVer];     // last query that sees it
-    float newc[kBatch][16];
+    float newc[kBatch][kRow];
     float gp[kBatch];  // live d(q_j, c*_j)
     int inval[kBatch];
     int nxt[kBatch];   // next query of the batch with the same c* (kBatch = none)
@@ -105,7 +106,10 @@ struct Scan2Shared {
     int st_h[16];      // exact-DFS stack (one lane)
     float st_box[16];
     uint32_t wkey[2][8];  // parallel exact DFS: per-wave next-improvement keys
+    float a2s[8][64];     // A2 scratch per wave: box terms by dimension, box' increments by depth
+    float a2i[8][64];
 };
+static_assert(sizeof(Scan2Shared) <= 160 * 1024, "LDS budget (160 KB per CU)");
 
 #ifdef GSC_STAMPS
 // diagnostic build: s_memtime per pipeline phase (cdna_hip_programming.md §7)
@@ -149,6 +153,8 @@ __device__ __forceinline__ uint32_t sum16(uint32_t v) {
     v += partner<2>(v);
     return v + partner<3>(v);
 }
+
+__device__ __forceinline__ int wave_of_lane() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
 // orders this wave's LDS accesses across lanes (lane-to-lane hand-off
 // through LDS inside one wave: without it the compiler may reorder them)
@@ -267,7 +273,21 @@ __device__ __forceinline__ void a1_query(const float (&creg)[8][D], const float*
 // ---------------------------------------------------------------------------
 template <int D, int LOGK, int NW>
 __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const float (*qrows)[16], QRec* recs, int wcol0,
-                                         int lane) {
+                                         int lane
+#ifdef GSC_STAMPS
+                                         , uint64_t* acc = nullptr, uint64_t* tl = nullptr
+#endif
+) {
+#ifdef GSC_STAMPS
+#define ASTAMP(k)                          \
+    if (acc) {                             \
+        const uint64_t t_ = stamp();       \
+        acc[k] += t_ - *tl;                \
+        *tl = t_;                          \
+    }
+#else
+#define ASTAMP(k)
+#endif
     constexpr int KW = LOGK >= 9 ? LOGK - 9 : 0;  // depths resolved at wave level
     const int l = lane & 15, gbase = lane & ~15;
     const int jj = j0 + (lane >> 4);
@@ -283,6 +303,7 @@ __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const 
     const int cstar = r.pos;
     const bool tie = nmin > 1 || r.tie;
     const float* q = qrows[jr];
+    ASTAMP(12)
     // sibling-subtree minimum at depth l
     uint32_t sib = 0xFFFFFFFFu;
     if (l < KW) {
@@ -313,24 +334,34 @@ __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const 
         }
     }
     const uint32_t farmask = (uint32_t)(__ballot(far) >> gbase) & 0xFFFFu;
-    // annBoxDistance(q, enclosing rect) in dimension order
+    ASTAMP(13)
+    // annBoxDistance(q, enclosing rect): lane l holds dimension l's term (or
+    // -1 = inside), summed below in dimension order; box' increments by depth
+    {
+        float term = -1.0f;
+        if (l < D) {
+            const float qd = q[l], blo = sh.t.bnd_lo[l], bhi = sh.t.bnd_hi[l];
+            const bool below = blo > qd, above = qd > bhi;
+            const float t = below ? fsub(blo, qd) : fsub(qd, bhi);
+            term = (below || above) ? fmul(t, t) : -1.0f;
+        }
+        sh.a2s[wave_of_lane()][lane] = term;
+        sh.a2i[wave_of_lane()][lane] = inc;
+    }
+    wave_lds_sync();
     float box = 0.0f;
+    {
+        const float* tv = &sh.a2s[wave_of_lane()][gbase];
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
-        const float qd = q[d];
-        if (sh.t.bnd_lo[d] > qd) {
-            const float t = fsub(sh.t.bnd_lo[d], qd);
-            box = fadd(box, fmul(t, t));
-        } else if (qd > sh.t.bnd_hi[d]) {
-            const float t = fsub(qd, sh.t.bnd_hi[d]);
-            box = fadd(box, fmul(t, t));
+        for (int d = 0; d < D; ++d) {
+            const float v = tv[d];
+            box = v >= 0.0f ? fadd(box, v) : box;
         }
     }
-    // box' at far steps, accumulated root -> leaf: box' = (cut^2 - bd^2) + box;
-    // B[l] = max over far steps at depth >= l
     float incs[LOGK];
 #pragma unroll
-    for (int k = 0; k < LOGK; ++k) incs[k] = __int_as_float(__shfl(__float_as_int(inc), gbase + k));
+    for (int k = 0; k < LOGK; ++k) incs[k] = sh.a2i[wave_of_lane()][gbase + k];
+    wave_lds_sync();  // the scratch is rewritten by this wave's next group
     float bp[LOGK];
 #pragma unroll
     for (int k = 0; k < LOGK; ++k) {
@@ -346,6 +377,7 @@ __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const 
         run = fmaxf(run, bp[k]);
         Bv = (l == k) ? run : Bv;
     }
+    ASTAMP(14)
     const bool ok = !far || (__uint_as_float(sib) > Bv);
     const bool gok = ((__ballot(!ok) >> gbase) & 0xFFFFull) == 0;
     const bool valid = !tie && __uint_as_float(gmin) <= FLT_MAX && gok;
@@ -363,7 +395,9 @@ __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const 
             R.farmask = farmask;
         }
     }
+    ASTAMP(15)
 }
+#undef ASTAMP
 
 // ---------------------------------------------------------------------------
 // Commit, step 1 (wave 0, lanes = queries j of the pending batch): online
@@ -755,7 +789,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
     double err = 0.0;
     int slow_total = 0, restarts = 0;
 #ifdef GSC_STAMPS
-    uint64_t acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tlast = stamp();
     acc[9] = tlast - t_kernel0;  // pass setup: tree build, registers, first queries
 #endif
@@ -828,7 +862,11 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
             STAMP(8)
 #pragma unroll 1
             for (int j0 = wave * 4; j0 < cur_n; j0 += 4 * NW)
-                a2_group<D, LOGK, NW>(sh, j0, cur_n, sh.q[cur_buf], sh.qrec[cur_buf], 0, lane);
+                a2_group<D, LOGK, NW>(sh, j0, cur_n, sh.q[cur_buf], sh.qrec[cur_buf], 0, lane
+#ifdef GSC_STAMPS
+                                      , acc, &tlast
+#endif
+                );
         }
         STAMP(2)
         lds_barrier();
@@ -1041,7 +1079,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
     }
 #ifdef GSC_STAMPS
     if (lane == 0)
-        for (int k = 0; k < 12; ++k) frp->stamps[wave * 12 + k] += acc[k];
+        for (int k = 0; k < 16; ++k) frp->stamps[wave * 16 + k] += acc[k];
 #endif
     if (tid == 0) {
         const double prev_err = pass == 0 ? 3.4028234663852886e+38 : frp->err;  // err := MaxSingle
