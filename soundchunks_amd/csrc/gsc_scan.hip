@@ -80,20 +80,21 @@ struct Scan2Shared {
     float dist[kMaxK];  // tree build scratch; live distances for the exact DFS
     float rate[kMaxK];  // Single(1/sqrt(cnts[not Odd(iter)])) by kd-leaf position
     float dfs_inc[kMaxK];  // exact DFS: per split node box' increment, sign = near child hi
-    float q[2][kBatch][16];
-    float qslow[16];       // the query resolved on its own after a failed commit
+    alignas(16) float q[2][kBatch][16];
+    alignas(16) float qslow[16];       // the query resolved on its own after a failed commit
     WaveRec wrec[8][kBatch + 1];  // column kBatch: the solo query
-    QRec qrec[2][kBatch];
+    alignas(16) QRec qrec[2][kBatch];
     QRec qsolo;
     // update log: entry e = wave-0 lane e (position in a VGPR, coordinates here)
-    float lg_c[64][kRow];
-    int pub_pos[64];
-    float pub_c[64][kRow];
+    alignas(16) float lg_c[64][kRow];
+    int pub_pos[64];       // log entries to fold into the registers (position, -1 = none)
+    alignas(16) float solo_c[kRow];    // coordinates of the solo query's centroid
+    double err_out;
     // commit of the pending batch: versions 0..63 = log entries, 64+j = after query j
     int vpos[kVer];
     int vfrom[kVer];   // first query that sees the version
     int vto[kVer];     // last query that sees it
-    float newc[kBatch][kRow];
+    alignas(16) float newc[kBatch][kRow];
     float gp[kBatch];  // live d(q_j, c*_j)
     int inval[kBatch];
     int nxt[kBatch];   // next query of the batch with the same c* (kBatch = none)
@@ -106,8 +107,8 @@ struct Scan2Shared {
     int st_h[16];      // exact-DFS stack (one lane)
     float st_box[16];
     uint32_t wkey[2][8];  // parallel exact DFS: per-wave next-improvement keys
-    float a2s[8][64];     // A2 scratch per wave: box terms by dimension, box' increments by depth
-    float a2i[8][64];
+    alignas(16) float a2s[8][64];     // A2 scratch per wave: box terms by dimension, box' increments by depth
+    alignas(16) float a2i[8][64];
 };
 static_assert(sizeof(Scan2Shared) <= 160 * 1024, "LDS budget (160 KB per CU)");
 
@@ -710,7 +711,7 @@ __device__ __forceinline__ void refresh(Scan2Shared& sh, float (&creg)[8][D], in
             if (s == slot) {
 #pragma unroll
                 for (int d = 0; d < D; ++d) {
-                    const float v = sh.pub_c[e][d];
+                    const float v = sh.lg_c[e][d];
                     creg[s][d] = lane == owner ? v : creg[s][d];
                 }
             }
@@ -725,6 +726,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
                                                          double tol, int pass) {
     constexpr int K = 1 << LOGK;
     constexpr int NW = K >= 512 ? K / 512 : 1;
+    constexpr int kErrWave = NW > 1 ? 1 : 0;  // residual + cluster ids (wave 0 keeps the log)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Scan2Shared& sh = *reinterpret_cast<Scan2Shared*>(smem);
     const int fi = blockIdx.x;
@@ -877,7 +879,9 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
             const uint64_t bad = __ballot(lane < P_n && sh.inval[lane] != 0);
             fj = bad ? __ffsll((long long)bad) - 1 : -1;
         }
-        if (wave == 0 && has_p) {
+        if (wave == kErrWave && has_p) {
+            // cluster ids, counts and the residual in query order (encoder.lpr:743:
+            // err += sqrt(best / colCount)) -- beside wave 0's log update
             const int k = fj >= 0 ? fj : P_n;
             const int j = lane;
             const bool cj = j < k;
@@ -886,9 +890,18 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
                 clusters[P_s + P_off + j] = R.id;
                 atomicAdd(&cnta[R.cstar], 1);
             }
-            // residual, in query order (encoder.lpr:743): err += sqrt(best / colCount)
             const float sq = cj ? __fsqrt_rn(sh.gp[j] / (float)D) : 0.0f;
-            for (int jj = 0; jj < k; ++jj) err += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(sq), jj));
+#pragma unroll
+            for (int jj = 0; jj < kBatch; ++jj) {
+                const double t = (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(sq), jj));
+                err = jj < k ? err + t : err;
+            }
+        }
+        if (wave == 0 && has_p) {
+            const int k = fj >= 0 ? fj : P_n;
+            const int j = lane;
+            const bool cj = j < k;
+            const QRec& R = sh.qrec[P_buf][P_off + (cj ? j : 0)];
             // the last committed update of each centroid becomes its log entry:
             // the entry already holding that centroid, else the r-th free entry
             const bool lastc = cj && sh.nxt[j] >= k;
@@ -954,10 +967,6 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
         if (wave == 0) {  // publish this iteration's commits (earlier ones are in the registers)
             const bool fresh_e = lg_pos >= 0 && lg_tag == it;
             sh.pub_pos[lane] = fresh_e ? lg_pos : -1;
-            if (fresh_e) {
-#pragma unroll
-                for (int d = 0; d < D; ++d) sh.pub_c[lane][d] = sh.lg_c[lane][d];
-            }
         }
         lds_barrier();
         STAMP(4)
@@ -1026,19 +1035,19 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
             for (int s = 0; s < 8; ++s)
                 if (s == slot && tid == owner) {
 #pragma unroll
-                    for (int d = 0; d < D; ++d) sh.pub_c[0][d] = creg[s][d];
+                    for (int d = 0; d < D; ++d) sh.solo_c[d] = creg[s][d];
                 }
             lds_barrier();
+            if (wave == kErrWave && lane == 0) err += (double)__fsqrt_rn(key / (float)D);
             if (wave == 0) {
                 if (lane == 0) {
                     const float rate = sh.rate[bpos];
                     for (int d = 0; d < D; ++d) {
-                        const float o = sh.pub_c[0][d];
-                        sh.pub_c[0][d] = fadd(o, fmul(fsub(sh.qslow[d], o), rate));
+                        const float o = sh.solo_c[d];
+                        sh.solo_c[d] = fadd(o, fmul(fsub(sh.qslow[d], o), rate));
                     }
                     atomicAdd(&cnta[bpos], 1);
                     clusters[solo_j] = sh.t.pidx[bpos];
-                    err += (double)__fsqrt_rn(key / (float)D);
                 }
                 wave_lds_sync();
                 const uint64_t hit = __ballot(lg_pos == bpos);
@@ -1047,9 +1056,9 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
                     lg_pos = bpos;
                     lg_tag = it;
 #pragma unroll
-                    for (int d = 0; d < D; ++d) sh.lg_c[e][d] = sh.pub_c[0][d];
+                    for (int d = 0; d < D; ++d) sh.lg_c[e][d] = sh.solo_c[d];
                 }
-                sh.pub_pos[lane] = lane == 0 ? bpos : -1;
+                sh.pub_pos[lane] = lane == e ? bpos : -1;
             }
             lds_barrier();
             refresh<D>(sh, creg, wave, lane);
@@ -1064,7 +1073,9 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
             break;
         }
     }
+    if (wave == kErrWave && lane == 0) sh.err_out = err;
     __syncthreads();
+    err = sh.err_out;
     // write back the live centroids and this pass's counts (cnts[Odd(iter)])
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
