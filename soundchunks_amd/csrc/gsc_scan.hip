@@ -426,15 +426,16 @@ __device__ __forceinline__ void vp_begin(Scan2Shared& sh, int qb, int off, int p
     wave_lds_sync();
 }
 
-// step k: pending query k against every lane's query / entry; log entries 2k, 2k+1
-__device__ __forceinline__ void vp_step(const Scan2Shared& sh, int qb, int off, int pn, int k, int lane, int lg_pos,
-                                        VPState& st) {
-    const int ck = k < pn ? sh.qrec[qb][off + k].cstar : -3;
-    if (k < lane && ck == st.cs) st.pred = 64 + k;
-    if (k > lane && ck == st.cs && st.nxt == kBatch) st.nxt = k;
+// step k (uniform): pending query k against every lane's query / entry, all
+// in registers (c*_k by readlane, the entries holding it by ballot)
+__device__ __forceinline__ void vp_step(int k, int lane, int lg_pos, VPState& st) {
+    const int ck = __builtin_amdgcn_readlane(st.cs, k);  // -2 past the batch: matches nothing
+    const bool same = ck == st.cs;
+    if (k < lane && same) st.pred = 64 + k;
+    if (k > lane && same && st.nxt == kBatch) st.nxt = k;
     if (ck == lg_pos && st.first == kBatch) st.first = k;  // lane as log entry: first query moving it
-    if (sh.vpos[2 * k] == st.cs) st.ie = min(st.ie, 2 * k);
-    if (sh.vpos[2 * k + 1] == st.cs) st.ie = min(st.ie, 2 * k + 1);
+    const uint64_t em = __ballot(lg_pos == ck);            // entries holding c*_k (lowest = ie_k)
+    if (lane == k && em) st.ie = __ffsll((long long)em) - 1;
 }
 
 // Commit, step 1 (wave 0, lanes = queries j of the pending batch): online
@@ -819,11 +820,11 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
 #pragma unroll 1
         for (int jj = 0; jj < cur_n; ++jj) {
             a1_query<D, LOGK>(creg, sh.q[cur_buf][jj], sh.wrec[wave][jj], wave, lane);
-            if (wave == 0 && has_p) vp_step(sh, P_buf, P_off, P_n, jj, lane, lg_pos, vst);
+            if (wave == 0 && has_p) vp_step(jj, lane, lg_pos, vst);
         }
         if (wave == 0 && has_p) {
 #pragma unroll 1
-            for (int k = cur_n; k < kBatch; ++k) vp_step(sh, P_buf, P_off, P_n, k, lane, lg_pos, vst);
+            for (int k = cur_n; k < kBatch; ++k) vp_step(k, lane, lg_pos, vst);
             vp_end<D, LOGK>(sh, P_buf, P_off, P_n, lane, lg_pos, vst);
         }
         STAMP(1)
