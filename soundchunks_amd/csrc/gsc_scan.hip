@@ -53,14 +53,39 @@ constexpr int kBatch = 32;         // queries per speculative batch (log window 
 constexpr int kVer = 64 + kBatch;  // centroid versions seen by a pending batch
 constexpr int kRow = 20;           // coordinate row stride of lane-indexed LDS rows (80 B: no b128 bank conflicts)
 
-struct WaveRec {      // A1 output per (wave, query)
+struct WaveRec {      // A1 output per (wave, query): raw values of the argmin lane L;
+                      // the winner's path minima are derived in A2 (rec_* below)
     uint32_t minbits; // wave minimum distance (f32 bits; distances are >= 0)
-    int tie;          // >= 2 leaves of this wave at the minimum
-    int pos;          // first kd-leaf position at the minimum
-    uint32_t sib[9];  // sibling-subtree minima on the path to pos:
-                      // [b] lane groups of 2^b lanes (b = 0..5),
-                      // [6] sibling slot, [7] other slot pair, [8] other slot quad
+    int lanebits;     // L | 256 if another lane of the wave also holds the minimum
+    uint32_t sl[6];   // lane L's sibling lane-group minima, groups of 2^b lanes (b = 0..5)
+    uint32_t b[8];    // lane L's 8 leaf distances (slots = kd leaves 8L .. 8L+7 of the wave)
 };
+
+// first slot of lane L at the wave minimum, and whether another slot ties it
+__device__ __forceinline__ int rec_slot(const WaveRec& r, bool* tie2) {
+    int ls = 7, lc = 0;
+#pragma unroll
+    for (int s = 7; s >= 0; --s) {
+        const bool e = r.b[s] == r.minbits;
+        lc += e ? 1 : 0;
+        ls = e ? s : ls;
+    }
+    *tie2 = lc > 1 || (r.lanebits >> 8) != 0;
+    return ls;
+}
+
+// sibling-subtree minimum on the path to slot ls: lane groups (idx 0..5),
+// sibling slot (6), other slot pair of the quad (7), other quad (8)
+__device__ __forceinline__ uint32_t rec_sib(const WaveRec& r, int ls, int idx) {
+    if (idx < 6) return r.sl[idx];
+    if (idx == 6) return r.b[ls ^ 1];
+    if (idx == 7) {
+        const int pb = (ls & 4) | ((ls & 2) ^ 2);
+        return min(r.b[pb], r.b[pb + 1]);
+    }
+    const int qb = (ls & 4) ^ 4;
+    return min(min(r.b[qb], r.b[qb + 1]), min(r.b[qb + 2], r.b[qb + 3]));
+}
 
 struct QRec {         // A2 output per query
     int valid;
@@ -236,28 +261,16 @@ __device__ __forceinline__ void a1_reduce(const float (&dv)[8], WaveRec& rec, in
     const uint64_t m = __ballot(lmin == wmin);
     const int L = __ffsll((long long)m) - 1;
     if (lane == L) {
-        int ls = 7, lc = 0;
-#pragma unroll
-        for (int s = 7; s >= 0; --s) {
-            const bool e = b[s] == lmin;
-            lc += e ? 1 : 0;
-            ls = e ? s : ls;
-        }
-        // in-lane sibling minima of slot ls: slot ls^1, pair (ls>>1)^1, quad (ls>>2)^1
-        const uint32_t pa = (ls & 4) ? ((ls & 2) ? b[6] : b[4]) : ((ls & 2) ? b[2] : b[0]);
-        const uint32_t pb = (ls & 4) ? ((ls & 2) ? b[7] : b[5]) : ((ls & 2) ? b[3] : b[1]);
         rec.minbits = wmin;
-        rec.tie = (__popcll(m) > 1 || lc > 1) ? 1 : 0;
-        rec.pos = p0 + ls;
-        rec.sib[0] = sl0;
-        rec.sib[1] = sl1;
-        rec.sib[2] = sl2;
-        rec.sib[3] = sl3;
-        rec.sib[4] = sl4;
-        rec.sib[5] = sl5;
-        rec.sib[6] = (ls & 1) ? pa : pb;
-        rec.sib[7] = (ls & 4) ? ((ls & 2) ? m45 : m67) : ((ls & 2) ? m01 : m23);
-        rec.sib[8] = (ls & 4) ? m03 : m47;
+        rec.lanebits = L | (__popcll(m) > 1 ? 256 : 0);
+        rec.sl[0] = sl0;
+        rec.sl[1] = sl1;
+        rec.sl[2] = sl2;
+        rec.sl[3] = sl3;
+        rec.sl[4] = sl4;
+        rec.sl[5] = sl5;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) rec.b[s] = b[s];
     }
 }
 
@@ -300,9 +313,12 @@ __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const 
     const uint32_t gmin = min16(mw);
     const uint32_t nmin = sum16((mw == gmin && l < NW) ? 1u : 0u);
     const int W = (int)min16((mw == gmin && l < NW) ? (uint32_t)l : 99u);
-    const WaveRec& r = sh.wrec[W < NW ? W : 0][wc];
-    const int cstar = r.pos;
-    const bool tie = nmin > 1 || r.tie;
+    const int Wv = W < NW ? W : 0;
+    const WaveRec& r = sh.wrec[Wv][wc];
+    bool tie2;
+    const int ls = rec_slot(r, &tie2);
+    const int cstar = (Wv * 64 + (r.lanebits & 255)) * 8 + ls;
+    const bool tie = nmin > 1 || tie2;
     const float* q = qrows[jr];
     ASTAMP(12)
     // sibling-subtree minimum at depth l
@@ -315,7 +331,7 @@ __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const 
             if ((w >> sh_) == want) sib = min(sib, sh.wrec[w][wc].minbits);
     } else if (l < LOGK) {
         const int idx = l <= LOGK - 4 ? (LOGK - 4 - l) : (l == LOGK - 3 ? 8 : (l == LOGK - 2 ? 7 : 6));
-        sib = r.sib[idx];
+        sib = rec_sib(r, ls, idx);
     }
     // split node at depth l on c*'s root path (ANNkd_split::ann_search)
     bool far = false;
@@ -853,8 +869,9 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
             while (won) {
                 const int jj = __ffsll((long long)won) - 1;
                 won &= won - 1;
-                const int p = sh.wrec[wave][jj].pos;
-                const int owner = (p >> 3) & 63, slot = p & 7;
+                const WaveRec& r = sh.wrec[wave][jj];
+                bool tie2;
+                const int owner = r.lanebits & 255, slot = rec_slot(r, &tie2);
 #pragma unroll
                 for (int s = 0; s < 8; ++s)
                     if (s == slot && lane == owner) {
