@@ -53,6 +53,16 @@ constexpr int kBatch = 32;         // queries per speculative batch (log window 
 constexpr int kVer = 64 + kBatch;  // centroid versions seen by a pending batch
 constexpr int kRow = 20;           // coordinate row stride of lane-indexed LDS rows (80 B: no b128 bank conflicts)
 
+// float minimum on f32 bit patterns (A1 values may be negative: the batch
+// queries' bounds are |c|^2 - 2 q.c; exact distances are >= +0, where this
+// equals the unsigned order).  fminf returns one operand bit for bit: no NaN
+// reaches it, and neither an fma chain started at |c|^2 >= +0 nor an exact
+// distance ever yields -0.
+__device__ __forceinline__ uint32_t fminb(uint32_t a, uint32_t b) {
+    return __float_as_uint(fminf(__uint_as_float(a), __uint_as_float(b)));
+}
+constexpr uint32_t kInfBits = 0x7F800000u;  // +inf: empty leaf / no value
+
 struct WaveRec {      // A1 output per (wave, query): raw values of the argmin lane L;
                       // the winner's path minima are derived in A2 (rec_* below)
     uint32_t minbits; // wave minimum distance (f32 bits; distances are >= 0)
@@ -81,10 +91,10 @@ __device__ __forceinline__ uint32_t rec_sib(const WaveRec& r, int ls, int idx) {
     if (idx == 6) return r.b[ls ^ 1];
     if (idx == 7) {
         const int pb = (ls & 4) | ((ls & 2) ^ 2);
-        return min(r.b[pb], r.b[pb + 1]);
+        return fminb(r.b[pb], r.b[pb + 1]);
     }
     const int qb = (ls & 4) ^ 4;
-    return min(min(r.b[qb], r.b[qb + 1]), min(r.b[qb + 2], r.b[qb + 3]));
+    return fminb(fminb(r.b[qb], r.b[qb + 1]), fminb(r.b[qb + 2], r.b[qb + 3]));
 }
 
 struct QRec {         // A2 output per query
@@ -106,6 +116,9 @@ struct Scan2Shared {
     float rate[kMaxK];  // Single(1/sqrt(cnts[not Odd(iter)])) by kd-leaf position
     float dfs_inc[kMaxK];  // exact DFS: per split node box' increment, sign = near child hi
     alignas(16) float q[2][kBatch][16];
+    alignas(16) float qm[2][kBatch][16];  // -2 q (exact), the A1 dot-product operand
+    float cnmax[8];
+    int fxl[kBatch];   // queries of the current batch re-certified exactly    // per wave: upper bound of |c|^2 over its live centroids (monotone within a pass)
     alignas(16) float qslow[16];       // the query resolved on its own after a failed commit
     WaveRec wrec[8][kBatch + 1];  // column kBatch: the solo query
     alignas(16) QRec qrec[2][kBatch];
@@ -173,6 +186,12 @@ __device__ __forceinline__ uint32_t min16(uint32_t v) {  // min over each aligne
     v = min(v, partner<2>(v));
     return min(v, partner<3>(v));
 }
+__device__ __forceinline__ uint32_t fmin16(uint32_t v) {  // float min over each aligned 16-lane row
+    v = fminb(v, partner<0>(v));
+    v = fminb(v, partner<1>(v));
+    v = fminb(v, partner<2>(v));
+    return fminb(v, partner<3>(v));
+}
 __device__ __forceinline__ uint32_t sum16(uint32_t v) {
     v += partner<0>(v);
     v += partner<1>(v);
@@ -236,28 +255,28 @@ __device__ __forceinline__ void a1_reduce(const float (&dv)[8], WaveRec& rec, in
     uint32_t b[8];
     const bool has = LOGK >= 9 || p0 < K;  // K >= 512: every lane holds 8 leaves
 #pragma unroll
-    for (int s = 0; s < 8; ++s) b[s] = has ? __float_as_uint(dv[s]) : 0xFFFFFFFFu;
-    const uint32_t m01 = min(b[0], b[1]), m23 = min(b[2], b[3]), m45 = min(b[4], b[5]), m67 = min(b[6], b[7]);
-    const uint32_t m03 = min(m01, m23), m47 = min(m45, m67);
-    const uint32_t lmin = min(m03, m47);
+    for (int s = 0; s < 8; ++s) b[s] = has ? __float_as_uint(dv[s]) : kInfBits;
+    const uint32_t m01 = fminb(b[0], b[1]), m23 = fminb(b[2], b[3]), m45 = fminb(b[4], b[5]), m67 = fminb(b[6], b[7]);
+    const uint32_t m03 = fminb(m01, m23), m47 = fminb(m45, m67);
+    const uint32_t lmin = fminb(m03, m47);
     // wave min-tree: partner group minima are the sibling subtrees on the path
     uint32_t v = lmin;
     const uint32_t sl0 = partner<0>(v);
-    v = min(v, sl0);
+    v = fminb(v, sl0);
     const uint32_t sl1 = partner<1>(v);
-    v = min(v, sl1);
+    v = fminb(v, sl1);
     const uint32_t sl2 = partner<2>(v);
-    v = min(v, sl2);
+    v = fminb(v, sl2);
     const uint32_t sl3 = partner<3>(v);
-    v = min(v, sl3);
+    v = fminb(v, sl3);
     // the two widest levels with the gfx950 row / half swaps: p[0] is this
     // lane's copy of the lower row (half), p[1] of the upper one
     const auto p16 = __builtin_amdgcn_permlane16_swap(v, v, false, false);
     const uint32_t sl4 = (lane & 16) ? p16[0] : p16[1];
-    v = min(p16[0], p16[1]);
+    v = fminb(p16[0], p16[1]);
     const auto p32 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
     const uint32_t sl5 = (lane & 32) ? p32[0] : p32[1];
-    const uint32_t wmin = min(p32[0], p32[1]);
+    const uint32_t wmin = fminb(p32[0], p32[1]);
     const uint64_t m = __ballot(lmin == wmin);
     const int L = __ffsll((long long)m) - 1;
     if (lane == L) {
@@ -283,11 +302,71 @@ __device__ __forceinline__ void a1_query(const float (&creg)[8][D], const float*
 }
 
 // ---------------------------------------------------------------------------
+// A1 of the batch queries: expanded-form distance bounds instead of the exact
+// sums.  A1 keeps s~ = |c|^2 + sum_d fma(-2 q_d, c_d, .) per leaf (16 VALU ops
+// instead of 48; the wave min-tree runs in float order); A2 adds |q|^2 once.
+// d~ = fl(|q|^2 + s~) differs from the reference's sequential f32 distance d
+// (ANN.dll @0x1800128b0) by at most eps(q) = (|q|^2 + M) * 2^-17, with
+// M >= |c|^2 over the live centroids: the 16 fma roundings are <= 32u(|c|^2 +
+// |q|^2) (every partial sum is within 2(|c|^2 + |q|^2) by Cauchy-Schwarz), the
+// two norms <= 16u each, the final add <= 2u, the reference's own sum <= 18u d
+// <= 36u(|c|^2 + |q|^2); u = 2^-24, total < 104u against the 128u used.  A2
+// certifies only with that margin; what it cannot decide is re-run exactly on
+// the same snapshot (fixup in part 2).  The committed distance g is always
+// recomputed exactly from c*'s coordinates (vp_end).
+// ---------------------------------------------------------------------------
+template <int D>
+__device__ __forceinline__ void a1_dist_x2(const float (&creg)[8][D], const float (&cn)[8], const float* __restrict__ qm0,
+                                           const float* __restrict__ qm1, float (&dv0)[8], float (&dv1)[8]) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        dv0[s] = cn[s];
+        dv1[s] = cn[s];
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const float m0 = qm0[d], m1 = qm1[d];
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            dv0[s] = __builtin_fmaf(m0, creg[s][d], dv0[s]);
+            dv1[s] = __builtin_fmaf(m1, creg[s][d], dv1[s]);
+        }
+    }
+}
+
+template <int D>
+__device__ __forceinline__ float norm2_x(const float* __restrict__ v) {  // |v|^2, any order (bounds only)
+    float n = 0.0f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) n = __builtin_fmaf(v[d], v[d], n);
+    return n;
+}
+
+// max over the wave of a non-negative float (bit order = value order)
+__device__ __forceinline__ float wave_max_nonneg(float x) {
+    uint32_t k = __float_as_uint(x);
+    k = max(k, partner<0>(k));
+    k = max(k, partner<1>(k));
+    k = max(k, partner<2>(k));
+    k = max(k, partner<3>(k));
+    k = max(k, partner<4>(k));
+    k = max((uint32_t)__builtin_amdgcn_readlane((int)k, 0), (uint32_t)__builtin_amdgcn_readlane((int)k, 32));
+    return __uint_as_float(k);
+}
+
+__device__ __forceinline__ float fsum16(float v) {  // sum over each aligned 16-lane row, uniform result
+    v = fadd(v, __uint_as_float(partner<0>(__float_as_uint(v))));
+    v = fadd(v, __uint_as_float(partner<1>(__float_as_uint(v))));
+    v = fadd(v, __uint_as_float(partner<2>(__float_as_uint(v))));
+    return fadd(v, __uint_as_float(partner<3>(__float_as_uint(v))));
+}
+
+// ---------------------------------------------------------------------------
 // A2: certificates of 4 queries per wave (16 lanes per query, lane = depth).
 // ---------------------------------------------------------------------------
-template <int D, int LOGK, int NW>
+template <int D, int LOGK, int NW, bool APPROX>
 __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const float (*qrows)[16], QRec* recs, int wcol0,
-                                         int lane
+                                         const int* jlist, int lane
 #ifdef GSC_STAMPS
                                          , uint64_t* acc = nullptr, uint64_t* tl = nullptr
 #endif
@@ -304,13 +383,15 @@ __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const 
 #endif
     constexpr int KW = LOGK >= 9 ? LOGK - 9 : 0;  // depths resolved at wave level
     const int l = lane & 15, gbase = lane & ~15;
-    const int jj = j0 + (lane >> 4);
-    const bool qa = jj < nq;
-    const int jr = qa ? jj : j0;  // safe index for inactive groups
+    const int t = j0 + (lane >> 4);  // query slot (an index into jlist when given)
+    const bool qa = t < nq;
+    const int tr = qa ? t : j0;  // safe slot for inactive groups
+    const int jr = jlist ? jlist[tr] : tr;
+    const int jj = jr;
     // global winner over the NW wave records (first wave at the minimum)
     const int wc = wcol0 + jr;
-    const uint32_t mw = (l < NW) ? sh.wrec[l][wc].minbits : 0xFFFFFFFFu;
-    const uint32_t gmin = min16(mw);
+    const uint32_t mw = (l < NW) ? sh.wrec[l][wc].minbits : kInfBits;
+    const uint32_t gmin = fmin16(mw);
     const uint32_t nmin = sum16((mw == gmin && l < NW) ? 1u : 0u);
     const int W = (int)min16((mw == gmin && l < NW) ? (uint32_t)l : 99u);
     const int Wv = W < NW ? W : 0;
@@ -322,13 +403,13 @@ __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const 
     const float* q = qrows[jr];
     ASTAMP(12)
     // sibling-subtree minimum at depth l
-    uint32_t sib = 0xFFFFFFFFu;
+    uint32_t sib = kInfBits;
     if (l < KW) {
         const int sh_ = KW - 1 - l;  // sibling wave group of W at depth l
         const int want = (W >> sh_) ^ 1;
 #pragma unroll
         for (int w = 0; w < NW; ++w)
-            if ((w >> sh_) == want) sib = min(sib, sh.wrec[w][wc].minbits);
+            if ((w >> sh_) == want) sib = fminb(sib, sh.wrec[w][wc].minbits);
     } else if (l < LOGK) {
         const int idx = l <= LOGK - 4 ? (LOGK - 4 - l) : (l == LOGK - 3 ? 8 : (l == LOGK - 2 ? 7 : 6));
         sib = rec_sib(r, ls, idx);
@@ -395,10 +476,27 @@ __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const 
         Bv = (l == k) ? run : Bv;
     }
     ASTAMP(14)
-    const bool ok = !far || (__uint_as_float(sib) > Bv);
+    const uint32_t m2 = fmin16(sib);  // every leaf except c*
+    bool ok, unique;
+    float m2lo;
+    if constexpr (APPROX) {
+        // A1 values are within eps of the reference's distances: certify with margins
+        const float qs = l < D ? q[l] : 0.0f;
+        const float qn = fsum16(__builtin_fmaf(qs, qs, 0.0f));
+        float M = 0.0f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) M = fmaxf(M, sh.cnmax[w]);
+        const float eps = fadd(fmul(fadd(qn, M), 0x1p-17f), 1e-37f);
+        ok = !far || (fsub(fadd(qn, __uint_as_float(sib)), eps) > Bv);
+        unique = fsub(__uint_as_float(m2), __uint_as_float(gmin)) > fadd(eps, eps);
+        m2lo = fsub(fadd(qn, __uint_as_float(m2)), eps);
+    } else {
+        ok = !far || (__uint_as_float(sib) > Bv);
+        unique = !tie;
+        m2lo = __uint_as_float(m2);
+    }
     const bool gok = ((__ballot(!ok) >> gbase) & 0xFFFFull) == 0;
-    const bool valid = !tie && __uint_as_float(gmin) <= FLT_MAX && gok;
-    const uint32_t m2 = min16(sib);  // every leaf except c*
+    const bool valid = unique && __uint_as_float(gmin) <= FLT_MAX && gok;
     if (qa) {
         QRec& R = recs[jj];
         if (l < LOGK) R.B[l] = Bv;
@@ -406,8 +504,8 @@ __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const 
             R.valid = valid ? 1 : 0;
             R.cstar = cstar;
             R.id = sh.t.pidx[cstar];
-            R.g = __uint_as_float(gmin);
-            R.m2 = __uint_as_float(m2);
+            R.g = __uint_as_float(gmin);  // exact mode only (the solo query); batch queries: vp_end
+            R.m2 = m2lo;
             R.rate = sh.rate[cstar];
             R.farmask = farmask;
         }
@@ -489,12 +587,10 @@ __device__ __forceinline__ void vp_end(Scan2Shared& sh, int qb, int off, int pn,
             float oc[D];
 #pragma unroll
             for (int d = 0; d < D; ++d) oc[d] = o[d];
-            float gpj = R.g;
-            bool okc = R.valid != 0;
-            if (pred >= 0) {
-                gpj = seqdist<D>(qv, oc);
-                okc = okc && gpj < R.m2;
-            }
+            // exact live distance to c* (its snapshot coordinates when unmoved;
+            // the A1 values of the batch are bounds only)
+            const float gpj = seqdist<D>(qv, oc);
+            const bool okc = R.valid != 0 && (pred < 0 || gpj < R.m2);
             const float rate = R.rate;
 #pragma unroll
             for (int d = 0; d < D; ++d) sh.newc[j][d] = fadd(oc[d], fmul(fsub(qv[d], oc[d]), rate));
@@ -715,9 +811,20 @@ __device__ __forceinline__ void dfs_parallel(Scan2Shared& sh, int tid, int lane,
 
 // fold published log entries into the owners' registers
 template <int D>
-__device__ __forceinline__ void refresh(Scan2Shared& sh, float (&creg)[8][D], int wave, int lane) {
+__device__ __forceinline__ void refresh(Scan2Shared& sh, float (&creg)[8][D], float (&cn)[8], float& cnmax, int wave,
+                                        int lane) {
     const int pp = sh.pub_pos[lane];
     uint64_t m = __ballot(pp >= 0 && (pp >> 9) == wave);
+    if (m) {
+        // the wave's norm bound only grows within a pass (A2 reads it for any earlier snapshot)
+        uint64_t mm = m;
+        while (mm) {
+            const int e = __ffsll((long long)mm) - 1;
+            mm &= mm - 1;
+            cnmax = fmaxf(cnmax, norm2_x<D>(sh.lg_c[e]));
+        }
+        if (lane == 0) sh.cnmax[wave] = cnmax;
+    }
     while (m) {
         const int e = __ffsll((long long)m) - 1;
         m &= m - 1;
@@ -731,8 +838,46 @@ __device__ __forceinline__ void refresh(Scan2Shared& sh, float (&creg)[8][D], in
                     const float v = sh.lg_c[e][d];
                     creg[s][d] = lane == owner ? v : creg[s][d];
                 }
+                const float nv = norm2_x<D>(sh.lg_c[e]);
+                cn[s] = lane == owner ? nv : cn[s];
             }
         }
+    }
+}
+
+// c*'s snapshot coordinates for the queries in qmask of batch buffer buf, written by the lane that owns c*
+// (the first wave / lane / slot at the minimum of the A1 records, as in A2)
+template <int D, int NW>
+__device__ __forceinline__ void write_cstar(Scan2Shared& sh, const float (&creg)[8][D], int buf, uint64_t qmask,
+                                            int wave, int lane) {
+    uint64_t won;
+    {
+        const bool act = (qmask >> lane) & 1ull;
+        const int jq = act ? lane : 0;
+        float gm = __builtin_inff();
+        int W = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const float m = __uint_as_float(sh.wrec[w][jq].minbits);
+            if (m < gm) {
+                gm = m;
+                W = w;
+            }
+        }
+        won = __ballot(act && W == wave);
+    }
+    while (won) {
+        const int jj = __ffsll((long long)won) - 1;
+        won &= won - 1;
+        const WaveRec& r = sh.wrec[wave][jj];
+        bool tie2;
+        const int owner = r.lanebits & 255, slot = rec_slot(r, &tie2);
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+            if (s == slot && lane == owner) {
+#pragma unroll
+                for (int d = 0; d < D; ++d) sh.qrec[buf][jj].o[d] = creg[s][d];
+            }
     }
 }
 
@@ -772,6 +917,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
     }
 
     float creg[8][D];
+    float cn[8];  // |c|^2 per register leaf (A1 bounds)
     const int p0 = tid * 8;
     bool nan_here = false;
 #pragma unroll
@@ -790,11 +936,24 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
 #pragma unroll
             for (int d = 0; d < D; ++d) creg[s][d] = 0.0f;
         }
+        cn[s] = norm2_x<D>(creg[s]);
     }
     if (nan_here) sh.any_nan = 1;
+    float cnmax;
+    {
+        float mx = 0.0f;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) mx = fmaxf(mx, cn[s]);
+        cnmax = wave_max_nonneg(nan_here ? 0.0f : mx);  // NaN passes leave for the generic kernel below
+        if (lane == 0) sh.cnmax[wave] = cnmax;
+    }
     // first batch's queries
     const int n0 = min(kBatch, N);
-    for (int k = tid; k < n0 * D; k += nthreads) sh.q[0][k / D][k % D] = X[k];
+    for (int k = tid; k < n0 * D; k += nthreads) {
+        const float x = X[k];
+        sh.q[0][k / D][k % D] = x;
+        sh.qm[0][k / D][k % D] = -2.0f * x;
+    }
     __syncthreads();
     if (uniform_int(sh.any_nan)) {
         // NaN centroids (yakmo 0/0 means) make ANN's early exits order dependent:
@@ -833,10 +992,19 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
         VPState vst;
         if (wave == 0 && has_p) vp_begin<D, LOGK>(sh, P_buf, P_off, P_n, vq_a1[0], lane, lg_pos, lg_tag, vst);
         STAMP(0)
+        // two queries per trip: one query's min-tree (a dependent DPP chain)
+        // overlaps the other's distance FMAs
 #pragma unroll 1
-        for (int jj = 0; jj < cur_n; ++jj) {
-            a1_query<D, LOGK>(creg, sh.q[cur_buf][jj], sh.wrec[wave][jj], wave, lane);
-            if (wave == 0 && has_p) vp_step(jj, lane, lg_pos, vst);
+        for (int jj = 0; jj < cur_n; jj += 2) {
+            const int j1 = jj + 1 < cur_n ? jj + 1 : jj;
+            float dv0[8], dv1[8];
+            a1_dist_x2<D>(creg, cn, sh.qm[cur_buf][jj], sh.qm[cur_buf][j1], dv0, dv1);
+            a1_reduce<LOGK>(dv0, sh.wrec[wave][jj], wave, lane);
+            a1_reduce<LOGK>(dv1, sh.wrec[wave][j1], wave, lane);
+            if (wave == 0 && has_p) {
+                vp_step(jj, lane, lg_pos, vst);
+                if (jj + 1 < cur_n) vp_step(jj + 1, lane, lg_pos, vst);
+            }
         }
         if (wave == 0 && has_p) {
 #pragma unroll 1
@@ -850,39 +1018,12 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
         if (has_p) v_check<D, LOGK>(sh, P_buf, P_off, P_n, tid, nthreads);
         STAMP(7)
         if (cur_n > 0) {
-            // c*'s snapshot coordinates, written by the wave that owns c*
-            uint64_t won;
-            {
-                const int jq = lane < cur_n ? lane : 0;
-                uint32_t gm = 0xFFFFFFFFu;
-                int W = 0;
-#pragma unroll
-                for (int w = 0; w < NW; ++w) {
-                    const uint32_t m = sh.wrec[w][jq].minbits;
-                    if (m < gm) {
-                        gm = m;
-                        W = w;
-                    }
-                }
-                won = __ballot(lane < cur_n && W == wave);
-            }
-            while (won) {
-                const int jj = __ffsll((long long)won) - 1;
-                won &= won - 1;
-                const WaveRec& r = sh.wrec[wave][jj];
-                bool tie2;
-                const int owner = r.lanebits & 255, slot = rec_slot(r, &tie2);
-#pragma unroll
-                for (int s = 0; s < 8; ++s)
-                    if (s == slot && lane == owner) {
-#pragma unroll
-                        for (int d = 0; d < D; ++d) sh.qrec[cur_buf][jj].o[d] = creg[s][d];
-                    }
-            }
+            // c*'s snapshot coordinates (and exact distance), written by the wave that owns c*
+            write_cstar<D, NW>(sh, creg, cur_buf, (1ull << cur_n) - 1ull, wave, lane);
             STAMP(8)
 #pragma unroll 1
             for (int j0 = wave * 4; j0 < cur_n; j0 += 4 * NW)
-                a2_group<D, LOGK, NW>(sh, j0, cur_n, sh.q[cur_buf], sh.qrec[cur_buf], 0, lane
+                a2_group<D, LOGK, NW, true>(sh, j0, cur_n, sh.q[cur_buf], sh.qrec[cur_buf], 0, nullptr, lane
 #ifdef GSC_STAMPS
                                       , acc, &tlast
 #endif
@@ -890,6 +1031,27 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
         }
         STAMP(2)
         lds_barrier();
+        if (cur_n > 0) {
+            // queries the approximate certificate could not decide: exact A1 + A2
+            // on the same snapshot (the registers change only in part 4)
+            const uint64_t fx = __ballot(lane < cur_n && sh.qrec[cur_buf][lane].valid == 0);
+            if (fx) {
+                const int nfx = __popcll(fx);
+                if (wave == 0 && ((fx >> lane) & 1ull)) sh.fxl[__popcll(fx & ((1ull << lane) - 1ull))] = lane;
+                uint64_t m = fx;
+                while (m) {
+                    const int jj = __ffsll((long long)m) - 1;
+                    m &= m - 1;
+                    a1_query<D, LOGK>(creg, sh.q[cur_buf][jj], sh.wrec[wave][jj], wave, lane);
+                }
+                lds_barrier();
+                write_cstar<D, NW>(sh, creg, cur_buf, fx, wave, lane);
+#pragma unroll 1
+                for (int j0 = wave * 4; j0 < nfx; j0 += 4 * NW)
+                    a2_group<D, LOGK, NW, false>(sh, j0, nfx, sh.q[cur_buf], sh.qrec[cur_buf], 0, sh.fxl, lane);
+                lds_barrier();
+            }
+        }
         STAMP(3)
         // ---- part 3: commit the valid prefix of the pending batch
         int fj = -1;
@@ -979,7 +1141,10 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
 #pragma unroll
             for (int e = 0; e < PE; ++e) {
                 const int k = tid + e * nthreads;
-                if (k < cur_n * D) sh.q[cur_buf][k / D][k % D] = pre[e];
+                if (k < cur_n * D) {
+                    sh.q[cur_buf][k / D][k % D] = pre[e];
+                    sh.qm[cur_buf][k / D][k % D] = -2.0f * pre[e];
+                }
             }
         }
         if (wave == 0) {  // publish this iteration's commits (earlier ones are in the registers)
@@ -989,7 +1154,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
         lds_barrier();
         STAMP(4)
         // ---- part 4: fold the log into the registers
-        refresh<D>(sh, creg, wave, lane);
+        refresh<D>(sh, creg, cn, cnmax, wave, lane);
         if (solo_j >= 0) {
             // the failed query on the live centroids: fresh distances and
             // certificate; exact DFS if the certificate still fails
@@ -997,8 +1162,8 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
             a1_query<D, LOGK>(creg, sh.qslow, sh.wrec[wave][kBatch], wave, lane);
             lds_barrier();
             if (wave == 0)
-                a2_group<D, LOGK, NW>(sh, 0, 1, reinterpret_cast<const float(*)[16]>(sh.qslow), &sh.qsolo, kBatch,
-                                      lane);
+                a2_group<D, LOGK, NW, false>(sh, 0, 1, reinterpret_cast<const float(*)[16]>(sh.qslow), &sh.qsolo, kBatch,
+                                             nullptr, lane);
             lds_barrier();
             int bpos;
             float key;
@@ -1079,7 +1244,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
                 sh.pub_pos[lane] = lane == e ? bpos : -1;
             }
             lds_barrier();
-            refresh<D>(sh, creg, wave, lane);
+            refresh<D>(sh, creg, cn, cnmax, wave, lane);
         }
         STAMP(5)
         if (nvq == 0 && cur_n == 0) {
