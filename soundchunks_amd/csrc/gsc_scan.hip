@@ -62,12 +62,16 @@ __device__ __forceinline__ uint32_t fminb(uint32_t a, uint32_t b) {
     return __float_as_uint(fminf(__uint_as_float(a), __uint_as_float(b)));
 }
 constexpr uint32_t kInfBits = 0x7F800000u;  // +inf: empty leaf / no value
+// f32 bits <-> signed-int order key (an involution): the cross-lane min-tree
+// runs on integer keys, so no DPP result needs an IEEE canonicalisation
+__device__ __forceinline__ int ordkey(uint32_t b) { return (int)(b ^ ((uint32_t)((int32_t)b >> 31) >> 1)); }
+__device__ __forceinline__ uint32_t keybits(int k) { return (uint32_t)ordkey((uint32_t)k); }
 
 struct WaveRec {      // A1 output per (wave, query): raw values of the argmin lane L;
                       // the winner's path minima are derived in A2 (rec_* below)
     uint32_t minbits; // wave minimum distance (f32 bits; distances are >= 0)
     int lanebits;     // L | 256 if another lane of the wave also holds the minimum
-    uint32_t sl[6];   // lane L's sibling lane-group minima, groups of 2^b lanes (b = 0..5)
+    uint32_t sl[6];   // lane L's sibling lane-group minima, groups of 2^b lanes (b = 0..5), as order keys
     uint32_t b[8];    // lane L's 8 leaf distances (slots = kd leaves 8L .. 8L+7 of the wave)
 };
 
@@ -87,7 +91,7 @@ __device__ __forceinline__ int rec_slot(const WaveRec& r, bool* tie2) {
 // sibling-subtree minimum on the path to slot ls: lane groups (idx 0..5),
 // sibling slot (6), other slot pair of the quad (7), other quad (8)
 __device__ __forceinline__ uint32_t rec_sib(const WaveRec& r, int ls, int idx) {
-    if (idx < 6) return r.sl[idx];
+    if (idx < 6) return keybits((int)r.sl[idx]);
     if (idx == 6) return r.b[ls ^ 1];
     if (idx == 7) {
         const int pb = (ls & 4) | ((ls & 2) ^ 2);
@@ -173,10 +177,11 @@ __device__ __forceinline__ uint64_t stamp() {
 // (valid for group-uniform inputs, which the reductions below guarantee)
 template <int B>
 __device__ __forceinline__ uint32_t partner(uint32_t v) {
-    if constexpr (B == 0) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-    if constexpr (B == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-    if constexpr (B == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
-    if constexpr (B == 3) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+    // every lane has a source lane in these patterns: no "old" value needed
+    if constexpr (B == 0) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
+    if constexpr (B == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
+    if constexpr (B == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true);  // row_half_mirror
+    if constexpr (B == 3) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true);  // row_mirror
     if constexpr (B == 4) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);                      // xor 16
     return 0u;
 }
@@ -248,49 +253,73 @@ __device__ __forceinline__ void a1_dist(const float (&creg)[8][D], const float* 
 }
 
 // wave min-tree over the lanes' 8 leaf distances -> the query's WaveRec
+struct A1Tree {
+    uint32_t b[8];  // this lane's leaf values (f32 bits)
+    uint32_t lmin;
+    int sl[6];      // partner lane-group minima (order keys)
+    uint64_t m;     // lanes at the wave minimum
+};
+
 template <int LOGK>
-__device__ __forceinline__ void a1_reduce(const float (&dv)[8], WaveRec& rec, int wave, int lane) {
+__device__ __forceinline__ A1Tree a1_tree(const float (&dv)[8], int wave, int lane) {
     constexpr int K = 1 << LOGK;
     const int p0 = (wave * 64 + lane) * 8;
-    uint32_t b[8];
+    A1Tree t;
     const bool has = LOGK >= 9 || p0 < K;  // K >= 512: every lane holds 8 leaves
 #pragma unroll
-    for (int s = 0; s < 8; ++s) b[s] = has ? __float_as_uint(dv[s]) : kInfBits;
-    const uint32_t m01 = fminb(b[0], b[1]), m23 = fminb(b[2], b[3]), m45 = fminb(b[4], b[5]), m67 = fminb(b[6], b[7]);
-    const uint32_t m03 = fminb(m01, m23), m47 = fminb(m45, m67);
-    const uint32_t lmin = fminb(m03, m47);
-    // wave min-tree: partner group minima are the sibling subtrees on the path
-    uint32_t v = lmin;
-    const uint32_t sl0 = partner<0>(v);
-    v = fminb(v, sl0);
-    const uint32_t sl1 = partner<1>(v);
-    v = fminb(v, sl1);
-    const uint32_t sl2 = partner<2>(v);
-    v = fminb(v, sl2);
-    const uint32_t sl3 = partner<3>(v);
-    v = fminb(v, sl3);
+    for (int s = 0; s < 8; ++s) t.b[s] = has ? __float_as_uint(dv[s]) : kInfBits;
+    const uint32_t m01 = fminb(t.b[0], t.b[1]), m23 = fminb(t.b[2], t.b[3]), m45 = fminb(t.b[4], t.b[5]),
+                   m67 = fminb(t.b[6], t.b[7]);
+    t.lmin = fminb(fminb(m01, m23), fminb(m45, m67));
+    // wave min-tree on order keys: partner group minima are the sibling subtrees on the path
+    const int key = ordkey(t.lmin);
+    int v = key;
+    t.sl[0] = (int)partner<0>((uint32_t)v);
+    v = min(v, t.sl[0]);
+    t.sl[1] = (int)partner<1>((uint32_t)v);
+    v = min(v, t.sl[1]);
+    t.sl[2] = (int)partner<2>((uint32_t)v);
+    v = min(v, t.sl[2]);
+    t.sl[3] = (int)partner<3>((uint32_t)v);
+    v = min(v, t.sl[3]);
     // the two widest levels with the gfx950 row / half swaps: p[0] is this
     // lane's copy of the lower row (half), p[1] of the upper one
-    const auto p16 = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    const uint32_t sl4 = (lane & 16) ? p16[0] : p16[1];
-    v = fminb(p16[0], p16[1]);
-    const auto p32 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    const uint32_t sl5 = (lane & 32) ? p32[0] : p32[1];
-    const uint32_t wmin = fminb(p32[0], p32[1]);
-    const uint64_t m = __ballot(lmin == wmin);
-    const int L = __ffsll((long long)m) - 1;
+    const auto p16 = __builtin_amdgcn_permlane16_swap((uint32_t)v, (uint32_t)v, false, false);
+    t.sl[4] = (int)((lane & 16) ? p16[0] : p16[1]);
+    v = min((int)p16[0], (int)p16[1]);
+    const auto p32 = __builtin_amdgcn_permlane32_swap((uint32_t)v, (uint32_t)v, false, false);
+    t.sl[5] = (int)((lane & 32) ? p32[0] : p32[1]);
+    const int wmin = min((int)p32[0], (int)p32[1]);
+    t.m = __ballot(key == wmin);
+    return t;
+}
+
+__device__ __forceinline__ void a1_store(const A1Tree& t, WaveRec& rec, int lane) {
+    const int L = __ffsll((long long)t.m) - 1;
     if (lane == L) {
-        rec.minbits = wmin;
-        rec.lanebits = L | (__popcll(m) > 1 ? 256 : 0);
-        rec.sl[0] = sl0;
-        rec.sl[1] = sl1;
-        rec.sl[2] = sl2;
-        rec.sl[3] = sl3;
-        rec.sl[4] = sl4;
-        rec.sl[5] = sl5;
+        rec.minbits = t.lmin;
+        rec.lanebits = L | (__popcll(t.m) > 1 ? 256 : 0);
 #pragma unroll
-        for (int s = 0; s < 8; ++s) rec.b[s] = b[s];
+        for (int i = 0; i < 6; ++i) rec.sl[i] = (uint32_t)t.sl[i];
+#pragma unroll
+        for (int s = 0; s < 8; ++s) rec.b[s] = t.b[s];
     }
+}
+
+template <int LOGK>
+__device__ __forceinline__ void a1_reduce(const float (&dv)[8], WaveRec& rec, int wave, int lane) {
+    a1_store(a1_tree<LOGK>(dv, wave, lane), rec, lane);
+}
+
+// two queries: both DPP chains are computed before either record store, so
+// their latencies overlap
+template <int LOGK>
+__device__ __forceinline__ void a1_reduce2(const float (&dv0)[8], const float (&dv1)[8], WaveRec& rec0, WaveRec& rec1,
+                                           int wave, int lane) {
+    const A1Tree t0 = a1_tree<LOGK>(dv0, wave, lane);
+    const A1Tree t1 = a1_tree<LOGK>(dv1, wave, lane);
+    a1_store(t0, rec0, lane);
+    a1_store(t1, rec1, lane);
 }
 
 template <int D, int LOGK>
@@ -604,6 +633,40 @@ __device__ __forceinline__ void vp_end(Scan2Shared& sh, int qb, int off, int pn,
 
 // Commit, step 2 (all threads): every (query, moved centroid) pair of the
 // pending batch -- the moved centroid must stay provably outside ANN's answer.
+// Lane = query j (lane & 31); wave / half-wave = a strided share of the
+// versions, so each version row is one LDS broadcast per half-wave and the
+// query row stays in registers.
+template <int D, int LOGK, int NW>
+__device__ __forceinline__ void v_check_q(Scan2Shared& sh, int qb, int off, int pn, int wave, int lane) {
+    const int j = lane & 31, hf = lane >> 5;
+    const bool act = j < pn;
+    const int jr = act ? j : 0;
+    const QRec& R = sh.qrec[qb][off + jr];
+    const int cs = R.cstar;
+    const uint32_t fm = R.farmask;
+    const float g = sh.gp[jr];
+    float q[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) q[d] = sh.q[qb][off + jr][d];
+    bool bad = false;
+#pragma unroll 1
+    for (int v = wave * 2 + hf; v < kVer; v += 2 * NW) {
+        const int vp = sh.vpos[v];
+        if (vp < 0 || !act || j < sh.vfrom[v] || j > sh.vto[v] || vp == cs) continue;
+        const float* c = v < 64 ? sh.lg_c[v] : sh.newc[v - 64];
+        float du = 0.0f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const float t = fsub(q[d], c[d]);
+            du = fadd(du, fmul(t, t));
+        }
+        const int lca = __clz(vp ^ cs) - (32 - LOGK);
+        const bool farl = (fm >> lca) & 1u;
+        if (!(du > g && (!farl || du > R.B[lca]))) bad = true;
+    }
+    if (bad) sh.inval[j] = 1;
+}
+
 template <int D, int LOGK>
 __device__ __forceinline__ void v_check(Scan2Shared& sh, int qb, int off, int pn, int tid, int nthreads) {
     const int npairs = pn * kVer;
@@ -999,8 +1062,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
             const int j1 = jj + 1 < cur_n ? jj + 1 : jj;
             float dv0[8], dv1[8];
             a1_dist_x2<D>(creg, cn, sh.qm[cur_buf][jj], sh.qm[cur_buf][j1], dv0, dv1);
-            a1_reduce<LOGK>(dv0, sh.wrec[wave][jj], wave, lane);
-            a1_reduce<LOGK>(dv1, sh.wrec[wave][j1], wave, lane);
+            a1_reduce2<LOGK>(dv0, dv1, sh.wrec[wave][jj], sh.wrec[wave][j1], wave, lane);
             if (wave == 0 && has_p) {
                 vp_step(jj, lane, lg_pos, vst);
                 if (jj + 1 < cur_n) vp_step(jj + 1, lane, lg_pos, vst);
@@ -1015,7 +1077,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
         lds_barrier();
         STAMP(6)
         // ---- part 2: check the pending batch; certificates of the current batch
-        if (has_p) v_check<D, LOGK>(sh, P_buf, P_off, P_n, tid, nthreads);
+        if (has_p) v_check_q<D, LOGK, NW>(sh, P_buf, P_off, P_n, wave, lane);
         STAMP(7)
         if (cur_n > 0) {
             // c*'s snapshot coordinates (and exact distance), written by the wave that owns c*
