@@ -153,6 +153,7 @@ struct Scan2Shared {
     alignas(16) float a2i[8][64];
 };
 static_assert(sizeof(Scan2Shared) <= 160 * 1024, "LDS budget (160 KB per CU)");
+static_assert(kRow >= 16 + 1, "log rows carry |c|^2 in their last float");
 
 #ifdef GSC_STAMPS
 // diagnostic build: s_memtime per pipeline phase (cdna_hip_programming.md §7)
@@ -878,21 +879,15 @@ __device__ __forceinline__ void refresh(Scan2Shared& sh, float (&creg)[8][D], fl
                                         int lane) {
     const int pp = sh.pub_pos[lane];
     uint64_t m = __ballot(pp >= 0 && (pp >> 9) == wave);
-    if (m) {
-        // the wave's norm bound only grows within a pass (A2 reads it for any earlier snapshot)
-        uint64_t mm = m;
-        while (mm) {
-            const int e = __ffsll((long long)mm) - 1;
-            mm &= mm - 1;
-            cnmax = fmaxf(cnmax, norm2_x<D>(sh.lg_c[e]));
-        }
-        if (lane == 0) sh.cnmax[wave] = cnmax;
-    }
+    const bool any = m != 0;
     while (m) {
         const int e = __ffsll((long long)m) - 1;
         m &= m - 1;
         const int p = __builtin_amdgcn_readlane(pp, e);
         const int owner = (p >> 3) & 63, slot = p & 7;
+        const float nv = sh.lg_c[e][kRow - 1];  // |c|^2, written with the entry
+        // the wave's norm bound only grows within a pass (A2 reads it for any earlier snapshot)
+        cnmax = fmaxf(cnmax, nv);
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
             if (s == slot) {
@@ -901,11 +896,11 @@ __device__ __forceinline__ void refresh(Scan2Shared& sh, float (&creg)[8][D], fl
                     const float v = sh.lg_c[e][d];
                     creg[s][d] = lane == owner ? v : creg[s][d];
                 }
-                const float nv = norm2_x<D>(sh.lg_c[e]);
                 cn[s] = lane == owner ? nv : cn[s];
             }
         }
     }
+    if (any && lane == 0) sh.cnmax[wave] = cnmax;
 }
 
 // c*'s snapshot coordinates for the queries in qmask of batch buffer buf, written by the lane that owns c*
@@ -1158,6 +1153,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
             if (lastc) {
 #pragma unroll
                 for (int d = 0; d < D; ++d) sh.lg_c[tgt][d] = sh.newc[j][d];
+                sh.lg_c[tgt][kRow - 1] = norm2_x<D>(sh.newc[j]);
                 sh.asg[tgt] = R.cstar;
             }
             wave_lds_sync();
@@ -1302,6 +1298,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
                     lg_tag = it;
 #pragma unroll
                     for (int d = 0; d < D; ++d) sh.lg_c[e][d] = sh.solo_c[d];
+                    sh.lg_c[e][kRow - 1] = norm2_x<D>(sh.solo_c);
                 }
                 sh.pub_pos[lane] = lane == e ? bpos : -1;
             }
