@@ -192,11 +192,18 @@ int Encoder::prepare(const uint8_t* wav, size_t len, std::string* err) {
     const int SC = sample_count_;
     filtered_.assign(size_t(ch), std::vector<double>(size_t(std::max(SC, 1)), 0.0));
     const uint8_t* d = wav + 44;
-    for (int i = 0; i < sc; ++i)
-        for (int c = 0; c < ch; ++c) {
-            const uint8_t* b = d + (size_t(i) * ch + c) * 2;
-            filtered_[c][i] = double(int16_t(uint16_t(b[0] | (b[1] << 8)))) / 32767.0;
-        }
+    // per-sample work in parallel blocks; every sequential f64 sum below keeps
+    // the reference's order (encoder.lpr:1374-1425)
+    constexpr int kBlk = 1 << 16;
+    const int nblk = (std::max(SC, sc) + kBlk - 1) / kBlk;
+    parallel_for(nblk, host_threads(), [&](int k) {
+        const int i1 = std::min(sc, (k + 1) * kBlk);
+        for (int i = k * kBlk; i < i1; ++i)
+            for (int c = 0; c < ch; ++c) {
+                const uint8_t* b = d + (size_t(i) * ch + c) * 2;
+                filtered_[c][i] = double(int16_t(uint16_t(b[0] | (b[1] << 8)))) / 32767.0;
+            }
+    });
     const int frame_count = int(fpc::ceil_pos(double(SC) / (double(sample_rate_) * (o.frame_length / 1000.0))));
     // ChunksPerFrame search only changes anything with -br (encoder.lpr:1337-1351)
     int cpf = o.chunks_per_frame;
@@ -222,14 +229,17 @@ int Encoder::prepare(const uint8_t* wav, size_t len, std::string* err) {
     }
     avg = std::sqrt(avg / double(SC * ch));
     std::vector<double> pw(static_cast<size_t>(std::max(SC, 1)));
+    parallel_for(nblk, host_threads(), [&](int k) {
+        const int i1 = std::min(SC, (k + 1) * kBlk);
+        for (int i = k * kBlk; i < i1; ++i) {
+            double s = 0.0;
+            for (int j = 0; j < ch; ++j) s += filtered_[j][i] * filtered_[j][i];
+            s = std::sqrt(s / double(ch));
+            pw[i] = 1.0 - (avg + (s - avg) * o.vfr);
+        }
+    });
     double total = 0.0;
-    for (int i = 0; i < SC; ++i) {
-        double s = 0.0;
-        for (int j = 0; j < ch; ++j) s += filtered_[j][i] * filtered_[j][i];
-        s = std::sqrt(s / double(ch));
-        pw[i] = 1.0 - (avg + (s - avg) * o.vfr);
-        total += pw[i];
-    }
+    for (int i = 0; i < SC; ++i) total += pw[i];
     const double per_frame = total / double(frame_count);
     fr_start_.clear();
     fr_end_.clear();

@@ -8,12 +8,17 @@
 //   device: yakmo seeding, KNNScanReduce, KNNFit search (gsc_kernels.hip)
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
 #include "../../include/soundchunks.h"
 
 namespace gsc {
+
+// host worker pool (gsc_runtime.cpp): fn(0..n-1) on up to `threads` threads
+void parallel_for(int n, int threads, const std::function<void(int)>& fn);
+int host_threads();
 
 struct FrameState {
     int index = 0, start = 0, sample_count = 0;

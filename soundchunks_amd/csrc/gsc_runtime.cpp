@@ -39,6 +39,37 @@ extern "C" hipError_t gsc_launch_knnfit(int CS, gsc::FitFrame* frames, int nfram
                                         const float* cand, const float* q, int* out, hipStream_t st);
 
 namespace gsc {
+
+void parallel_for(int n, int threads, const std::function<void(int)>& fn) {
+    if (threads <= 1 || n <= 1) {
+        for (int i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    std::atomic<int> next{0};
+    std::vector<std::thread> pool;
+    const int t = std::min(threads, n);
+    pool.reserve(size_t(t));
+    for (int k = 0; k < t; ++k)
+        pool.emplace_back([&] {
+            for (;;) {
+                const int i = next.fetch_add(1);
+                if (i >= n) break;
+                fn(i);
+            }
+        });
+    for (auto& th : pool) th.join();
+}
+
+int host_threads() {
+    static int n = [] {
+        const char* e = std::getenv("GSC_HOST_THREADS");
+        if (e && std::atoi(e) > 0) return std::atoi(e);
+        const unsigned hc = std::thread::hardware_concurrency();
+        return int(std::min(16u, std::max(1u, hc)));
+    }();
+    return n;
+}
+
 namespace {
 
 thread_local std::string t_err;
@@ -97,36 +128,6 @@ struct DevBuf {
         return hipMalloc(&p, sizeof(T) * std::max<size_t>(count, 1));
     }
 };
-
-void parallel_for(int n, int threads, const std::function<void(int)>& fn) {
-    if (threads <= 1 || n <= 1) {
-        for (int i = 0; i < n; ++i) fn(i);
-        return;
-    }
-    std::atomic<int> next{0};
-    std::vector<std::thread> pool;
-    const int t = std::min(threads, n);
-    pool.reserve(size_t(t));
-    for (int k = 0; k < t; ++k)
-        pool.emplace_back([&] {
-            for (;;) {
-                const int i = next.fetch_add(1);
-                if (i >= n) break;
-                fn(i);
-            }
-        });
-    for (auto& th : pool) th.join();
-}
-
-int host_threads() {
-    static int n = [] {
-        const char* e = std::getenv("GSC_HOST_THREADS");
-        if (e && std::atoi(e) > 0) return std::atoi(e);
-        const unsigned hc = std::thread::hardware_concurrency();
-        return int(std::min(16u, std::max(1u, hc)));
-    }();
-    return n;
-}
 
 // IntPower(10.0, -Precision) (encoder.lpr:761)
 double scan_tolerance(int precision) {
@@ -490,31 +491,38 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
     {
         std::vector<int> Rs(static_cast<size_t>(nfr)), Nq(static_cast<size_t>(nfr));
         std::vector<float> eps(static_cast<size_t>(nfr));
-        std::vector<float> cand, q;
+        std::vector<size_t> coff(size_t(nfr) + 1, 0), qoff(size_t(nfr) + 1, 0);
+        for (int i = 0; i < nfr; ++i) {
+            Rs[i] = frames[i].r;
+            Nq[i] = frames[i].n;
+            coff[i + 1] = coff[i] + size_t(frames[i].r) * cs;
+            qoff[i + 1] = qoff[i] + frames[i].src.size();
+        }
+        std::vector<float> cand(coff[nfr]), q(qoff[nfr]);
         const int bd = opt_.chunk_bit_depth;
         const int obd = (1 << (bd - 1)) - 1;
-        for (int i = 0; i < nfr; ++i) {
-            FrameState& f = frames[i];
+        parallel_for(nfr, host_threads(), [&](int i) {
+            const FrameState& f = frames[i];
             const double law = 1.0 / double(f.atten_div);
-            Rs[i] = f.r;
-            Nq[i] = f.n;
             // epsilon (encoder.lpr:940-943), accumulated in Single
             float acc = 1.0f;
             for (int j = 0; j <= 15; ++j) acc = float(double(acc) + double(j) * law);
             const float e1 = 1.0f / (float(1 << bd) * acc);
             const float e2 = float(1.0 / 32767.0);
             eps[i] = e1 > e2 ? e1 : e2;
+            float* cp = cand.data() + coff[i];
             for (int c = 0; c < f.r; ++c) {
                 double coeff = 1.0;
                 for (int a = 0; a <= f.ratten[c]; ++a) coeff += double(a) * law;
                 for (int j = 0; j < cs; ++j) {
                     double v = double(f.rdst[size_t(c) * cs + j]) / (double(obd) * coeff);
                     v = std::min(1.0, std::max(-1.0, v));
-                    cand.push_back(float(v));
+                    *cp++ = float(v);
                 }
             }
-            for (size_t k = 0; k < f.src.size(); ++k) q.push_back(float(f.src[k]));
-        }
+            float* qp = q.data() + qoff[i];
+            for (size_t k = 0; k < f.src.size(); ++k) qp[k] = float(f.src[k]);
+        });
         std::vector<int> best;
         if (run_knnfit_batch(cs, Rs, Nq, eps, cand, q, &best, &knn_ms) != 0) {
             *err = t_err;
