@@ -190,12 +190,13 @@ int Encoder::prepare(const uint8_t* wav, size_t len, std::string* err) {
     block_ = under * (cs - o.chunk_blend);
     sample_count_ = ((sc - 1) / block_ + 1) * block_;  // Pascal div truncates
     const int SC = sample_count_;
-    filtered_.assign(size_t(ch), std::vector<double>(size_t(std::max(SC, 1)), 0.0));
+    filtered_.resize(size_t(ch));
+    for (auto& v : filtered_) v.resize(size_t(std::max(SC, 1)));  // no fill: the workers below write every sample
     const uint8_t* d = wav + 44;
     // per-sample work in parallel blocks; every sequential f64 sum below keeps
     // the reference's order (encoder.lpr:1374-1425)
     constexpr int kBlk = 1 << 16;
-    const int nblk = (std::max(SC, sc) + kBlk - 1) / kBlk;
+    const int nblk = (std::max({SC, sc, 1}) + kBlk - 1) / kBlk;
     parallel_for(nblk, host_threads(), [&](int k) {
         const int i1 = std::min(sc, (k + 1) * kBlk);
         for (int i = k * kBlk; i < i1; ++i)
@@ -203,6 +204,9 @@ int Encoder::prepare(const uint8_t* wav, size_t len, std::string* err) {
                 const uint8_t* b = d + (size_t(i) * ch + c) * 2;
                 filtered_[c][i] = double(int16_t(uint16_t(b[0] | (b[1] << 8)))) / 32767.0;
             }
+        const int z1 = std::min(std::max(SC, 1), (k + 1) * kBlk);  // zero padding past the WAV end
+        for (int i = std::max(sc, k * kBlk); i < z1; ++i)
+            for (int c = 0; c < ch; ++c) filtered_[c][i] = 0.0;
     });
     const int frame_count = int(fpc::ceil_pos(double(SC) / (double(sample_rate_) * (o.frame_length / 1000.0))));
     // ChunksPerFrame search only changes anything with -br (encoder.lpr:1337-1351)
@@ -245,9 +249,9 @@ int Encoder::prepare(const uint8_t* wav, size_t len, std::string* err) {
     fr_end_.clear();
     int next = 0;
     double cur = 0.0;
-    for (int i = 0; i < SC; ++i) {
+    for (int i = 0, r = 0; i < SC; ++i, r = (r + 1 == block_) ? 0 : r + 1) {  // r = i mod block_
         cur += pw[i];
-        if ((i % block_ == 0) && (cur >= per_frame)) {
+        if ((r == 0) && (cur >= per_frame)) {
             fr_start_.push_back(next);
             fr_end_.push_back(i - 1);
             cur = 0.0;

@@ -9,12 +9,35 @@
 #pragma once
 #include <cstdint>
 #include <functional>
+#include <memory>
+#include <utility>
 #include <string>
 #include <vector>
 
 #include "../../include/soundchunks.h"
 
 namespace gsc {
+
+// allocator whose value-initialisation is a no-op: large host buffers are
+// filled (and first touched) by the parallel workers, not by one thread
+template <typename T>
+struct NoInitAlloc : std::allocator<T> {
+    template <typename U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <typename U>
+    NoInitAlloc(const NoInitAlloc<U>&) {}
+    template <typename U>
+    void construct(U* p) noexcept {
+        ::new (static_cast<void*>(p)) U;
+    }
+    template <typename U, typename... A>
+    void construct(U* p, A&&... a) {
+        ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+    }
+};
 
 // host worker pool (gsc_runtime.cpp): fn(0..n-1) on up to `threads` threads
 void parallel_for(int n, int threads, const std::function<void(int)>& fn);
@@ -79,7 +102,7 @@ class Encoder {
     int channels_ = 0, sample_rate_ = 0;
     int sample_count_ = 0;
     int block_ = 1;
-    std::vector<std::vector<double>> filtered_;  // [ch][sample] = s / 32767
+    std::vector<std::vector<double, NoInitAlloc<double>>> filtered_;  // [ch][sample] = s / 32767
     std::vector<int> fr_start_, fr_end_;
 };
 

@@ -36,7 +36,7 @@ constexpr int kYThreads = 64 + kYBlock;  // wave 0: picks + prefix chain
 constexpr int kYBits = 262144 / 32;   // chosen-point bitmap in LDS (N <= 262144)
 
 struct YakmoShared {
-    float ring[2][kYBlock];    // d0 of the last two blocks (chain input)
+    alignas(16) float ring[2][kYBlock];    // d0 of the last two blocks (chain input)
     uint32_t chosen[kYBits];
     int cursor[kMaxK];         // stable counting sort of the final assignment
     float c[32];               // current seed
@@ -137,16 +137,24 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
                     const int base = (b - 1) * kYBlock;
 #pragma unroll
                     for (int k = 0; k < kYBlock / 64; ++k) {
-                        const int v = __float_as_int(sh.ring[(b - 1) & 1][k * 64 + lane]);
                         const int cnt = min(64, N - (base + k * 64));
                         if (cnt == 64) {
-                            // 64 v_readlane (immediate lanes) into SGPRs, then the dependent adds back to back
-                            int sv[64];
+                            // the 64 values as LDS broadcast reads into VGPRs (every lane loads
+                            // the same row), then the dependent adds back to back: no VALU
+                            // readlane per point on the critical chain
+                            const float4* row = reinterpret_cast<const float4*>(&sh.ring[(b - 1) & 1][k * 64]);
+                            float4 sv[16];
 #pragma unroll
-                            for (int l = 0; l < 64; ++l) sv[l] = __builtin_amdgcn_readlane(v, l);
+                            for (int l = 0; l < 16; ++l) sv[l] = row[l];
 #pragma unroll
-                            for (int l = 0; l < 64; ++l) run = fa(run, __int_as_float(sv[l]));
+                            for (int l = 0; l < 16; ++l) {
+                                run = fa(run, sv[l].x);
+                                run = fa(run, sv[l].y);
+                                run = fa(run, sv[l].z);
+                                run = fa(run, sv[l].w);
+                            }
                         } else {
+                            const int v = __float_as_int(sh.ring[(b - 1) & 1][k * 64 + lane]);
                             for (int l = 0; l < cnt; ++l) run = fa(run, __int_as_float(__builtin_amdgcn_readlane(v, l)));
                         }
                         if (cnt > 0 && lane == 0) ckpt[((base + k * 64) >> 6)] = run;
