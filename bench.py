@@ -155,7 +155,9 @@ def main():
                    "parallelism": f"frame-sharded x{ws}"},
         "realtime_x": round(value / (rate * ch / 1e6), 2),
         "roofline": {"bound": "valu", "kernel": "scan_batch_kernel", "achieved": round(achieved, 4),
-                     "peak": VALU_F32_PEAK_TOPS, "unit": "Tops/s (non-fused f32 VALU; bit-exactness rules out FMA/MFMA)",
+                     "peak": VALU_F32_PEAK_TOPS, "unit": "Tops/s (algorithmic: the reference's sub+mul+add per leaf coordinate, 6K ops per sample per "
+                             "pass; peak = non-fused f32 VALU issue rate; the kernel itself bounds distances with one "
+                             "fma per coordinate and recomputes exactly only what it commits)",
                      "frac": round(achieved / VALU_F32_PEAK_TOPS, 5),
                      "traffic": None if traffic is None else round(traffic),
                      "hbm_gbs": None if traffic is None else round(traffic / avg_launch_s / 1e9, 2),

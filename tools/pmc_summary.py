@@ -1,7 +1,7 @@
 """Build profiles/<round>/pmc_summary.json from two rocprofv3 --pmc CSV passes
 (FETCH_SIZE and WRITE_SIZE collected in separate runs, MI355X_MICROARCH.md):
 
-    python tools/pmc_summary.py FETCH.csv WRITE.csv FRAMES "bench.py --seconds 256" > profiles/r01/pmc_summary.json
+    python tools/pmc_summary.py FETCH.{csv,db} WRITE.{csv,db} FRAMES "bench.py --seconds 256" > profiles/r01/pmc_summary.json
 
 Per kernel: launches, KiB per launch as reported, HBM bytes per launch with
 the gfx950 correction (FETCH_SIZE x 2 for wide coalesced reads) and per frame.
@@ -20,6 +20,16 @@ def short(name):
 
 def load(path, counter):
     acc = defaultdict(lambda: [0, 0.0])
+    if path.endswith(".db"):  # rocpd database (rocprofv3's default output on this image)
+        import sqlite3
+
+        c = sqlite3.connect(path)
+        for name, value in c.execute("select kernel_name, value from counters_collection where counter_name = ?",
+                                     (counter,)):
+            k = short(name)
+            acc[k][0] += 1
+            acc[k][1] += float(value)
+        return acc
     with open(path, newline="") as f:
         for row in csv.DictReader(f):
             if row["Counter_Name"] != counter:
