@@ -96,7 +96,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
                                                                   float* __restrict__ Call, int* __restrict__ i_scratch,
                                                                   float* __restrict__ f_scratch,
                                                                   const float* __restrict__ rate_tab, double tol,
-                                                                  int pass, int only_flagged) {
+                                                                  int max_passes, int only_flagged) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     ScanShared& sh = *reinterpret_cast<ScanShared*>(smem);
     const int fi = blockIdx.x;
@@ -104,6 +104,8 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
     ReduceFrame* frp = frames + fi;
     if (uniform_int(frp->done)) return;
     if (only_flagged && !uniform_int(frp->generic)) return;  // the batched kernel ran this pass
+    const int pass = uniform_int(frp->iters);  // frames advance on their own pass counts
+    if (pass >= max_passes) return;
     const int N = uniform_int(frp->N), K = uniform_int(frp->K);
     const float* __restrict__ X = uniform_ptr(Xall + frp->x_off);
     float* C = uniform_ptr(Call + frp->c_off);
@@ -474,7 +476,7 @@ __global__ __launch_bounds__(256) void knnfit_kernel(FitFrame* __restrict__ fram
 using namespace gsc;
 
 extern "C" hipError_t gsc_launch_scan_pass(int D, ReduceFrame* frames, int nframes, int K, const float* X, float* C,
-                                           int* is, float* fs, const float* rate_tab, double tol, int pass,
+                                           int* is, float* fs, const float* rate_tab, double tol, int max_passes,
                                            int only_flagged, hipStream_t st) {
     const int waves = (K + 64 * kScanSlots - 1) / (64 * kScanSlots);
     dim3 grid(nframes), block(64 * waves);
@@ -482,11 +484,11 @@ extern "C" hipError_t gsc_launch_scan_pass(int D, ReduceFrame* frames, int nfram
     switch (D) {
     case 8:
         (void)hipFuncSetAttribute((const void*)scan_pass_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-        hipLaunchKernelGGL(scan_pass_kernel<8>, grid, block, shm, st, frames, nframes, X, C, is, fs, rate_tab, tol, pass, only_flagged);
+        hipLaunchKernelGGL(scan_pass_kernel<8>, grid, block, shm, st, frames, nframes, X, C, is, fs, rate_tab, tol, max_passes, only_flagged);
         break;
     case 16:
         (void)hipFuncSetAttribute((const void*)scan_pass_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-        hipLaunchKernelGGL(scan_pass_kernel<16>, grid, block, shm, st, frames, nframes, X, C, is, fs, rate_tab, tol, pass, only_flagged);
+        hipLaunchKernelGGL(scan_pass_kernel<16>, grid, block, shm, st, frames, nframes, X, C, is, fs, rate_tab, tol, max_passes, only_flagged);
         break;
     default: return hipErrorInvalidValue;
     }

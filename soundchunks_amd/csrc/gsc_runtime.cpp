@@ -25,10 +25,10 @@
 extern "C" hipError_t gsc_launch_yakmo(int D, const gsc::ReduceFrame* frames, int nframes, const float* X, float* C,
                                        float* fs, int* is, uint32_t* bits, hipStream_t st);
 extern "C" hipError_t gsc_launch_scan_pass(int D, gsc::ReduceFrame* frames, int nframes, int K, const float* X,
-                                           float* C, int* is, float* fs, const float* rate_tab, double tol, int pass,
+                                           float* C, int* is, float* fs, const float* rate_tab, double tol, int max_passes,
                                            int only_flagged, hipStream_t st);
 extern "C" hipError_t gsc_launch_scan_batch(int D, int logk, gsc::ReduceFrame* frames, int nframes, const float* X,
-                                            float* C, int* is, const float* rate_tab, double tol, int pass,
+                                            float* C, int* is, const float* rate_tab, double tol, int max_passes,
                                             hipStream_t st);
 extern "C" hipError_t gsc_launch_atten(int cs, gsc::DspFrame* frames, int nframes, const double* samp, int64_t span,
                                        int ch, int obd, hipStream_t st);
@@ -152,9 +152,13 @@ bool batched_scan_shape(int D, int K) {
     return (D == 8 || D == 16) && K >= 256 && K <= 4096 && (K & (K - 1)) == 0;
 }
 
-// all KNNScanReduce passes of a batch: one launch per pass, converged frames
-// exit early; the generic launch after a batched one only runs the frames the
-// batched kernel handed over (NaN centroids)
+// launch rounds of launch_scan_passes since the last reset (bench: launches
+// of the dominant kernel)
+std::atomic<int> g_scan_rounds{0};
+
+// all KNNScanReduce passes of a batch; converged frames exit early, the
+// generic launch after a batched one only runs the frames the batched kernel
+// handed over (NaN centroids)
 hipError_t launch_scan_passes(int D, ReduceFrame* dfr, int nf, int K, const float* X, float* C, int* is, float* fs,
                               const float* rate, int precision) {
     const double tol = scan_tolerance(precision);
@@ -163,13 +167,24 @@ hipError_t launch_scan_passes(int D, ReduceFrame* dfr, int nf, int K, const floa
     while ((1 << logk) < K) ++logk;
     int max_passes = kMaxScanIters;
     if (const char* e = std::getenv("GSC_SCAN_MAX_PASSES")) max_passes = std::max(1, std::min(kMaxScanIters, std::atoi(e)));
-    for (int pass = 0; pass < max_passes; ++pass) {
+    // every launch advances each live frame by at least one pass (the batched
+    // kernel runs a frame until it converges or meets a NaN pass, which the
+    // generic launch then takes), so max_passes rounds always suffice
+    std::vector<int32_t> done(static_cast<size_t>(nf));
+    for (int round = 0; round < max_passes; ++round) {
         if (batched) {
-            const hipError_t e = gsc_launch_scan_batch(D, logk, dfr, nf, X, C, is, rate, tol, pass, nullptr);
+            const hipError_t e = gsc_launch_scan_batch(D, logk, dfr, nf, X, C, is, rate, tol, max_passes, nullptr);
             if (e != hipSuccess) return e;
         }
-        const hipError_t e = gsc_launch_scan_pass(D, dfr, nf, K, X, C, is, fs, rate, tol, pass, batched ? 1 : 0, nullptr);
+        const hipError_t e = gsc_launch_scan_pass(D, dfr, nf, K, X, C, is, fs, rate, tol, max_passes, batched ? 1 : 0, nullptr);
         if (e != hipSuccess) return e;
+        g_scan_rounds.fetch_add(1);
+        if (!batched) continue;  // the generic kernel runs one pass per round
+        // stop once every frame is done (read back the done flags only)
+        const hipError_t c = hipMemcpy2D(done.data(), sizeof(int32_t), &dfr[0].done, sizeof(ReduceFrame),
+                                         sizeof(int32_t), size_t(nf), hipMemcpyDeviceToHost);
+        if (c != hipSuccess) return c;
+        if (std::all_of(done.begin(), done.end(), [](int32_t v) { return v != 0; })) break;
     }
     return hipSuccess;
 }
@@ -467,6 +482,7 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
     if (!red_idx.empty()) {
         std::vector<float> C;
         std::vector<int> cl, it, sl;
+        g_scan_rounds.store(0);
         if (run_reduce_batch_dev(D, K, opt_.precision, Ns, red_xoff, dFeat.p, &C, &cl, &it, &sl, &restarts, &yak_ms,
                                  &scan_ms) != 0) {
             *err = t_err;
@@ -560,7 +576,7 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
         long long pp = 0;
         for (auto& f : frames) pp += (long long)f.scan_iters * f.n;
         tim->scan_point_passes = pp;
-        tim->scan_launches = red_idx.empty() ? 0 : kMaxScanIters;
+        tim->scan_launches = g_scan_rounds.exchange(0);
         tim->knnfit_launches = 1;
         long long cand = 0;
         for (auto& f : frames) cand += (long long)f.n * 4 * f.r_before_prune;

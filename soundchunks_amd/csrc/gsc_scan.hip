@@ -146,6 +146,7 @@ struct Scan2Shared {
     int slow_pos;
     float slow_key;
     int any_nan;
+    int pass_done;     // end of pass: the frame converged (or hands the next pass over)
     int st_h[16];      // exact-DFS stack (one lane)
     float st_box[16];
     uint32_t wkey[2][8];  // parallel exact DFS: per-wave next-improvement keys
@@ -943,7 +944,7 @@ template <int D, int LOGK>
 __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict__ frames, int nframes,
                                                          const float* __restrict__ Xall, float* __restrict__ Call,
                                                          int* __restrict__ i_scratch, const float* __restrict__ rate_tab,
-                                                         double tol, int pass) {
+                                                         double tol, int max_passes) {
     constexpr int K = 1 << LOGK;
     constexpr int NW = K >= 512 ? K / 512 : 1;
     constexpr int kErrWave = NW > 1 ? 1 : 0;  // residual + cluster ids (wave 0 keeps the log)
@@ -962,6 +963,10 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nthreads = 64 * NW;
 
+    // All of the frame's passes run in this launch (the pass index lives in
+    // the frame descriptor), so a frame never waits for the slowest frame of a
+    // pass; a NaN pass returns and the generic kernel takes that pass over.
+    for (int pass = uniform_int(frp->iters); pass < max_passes; ++pass) {
 #ifdef GSC_STAMPS
     const uint64_t t_kernel0 = stamp();
 #endif
@@ -1342,6 +1347,13 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
         frp->restarts += restarts;
         frp->err = err;
         frp->done = (diff <= tol || pass + 1 >= kMaxScanIters || frp->loop_iters < 0) ? 1 : 0;
+        sh.pass_done = frp->done;
+    }
+    // the next pass's tree build and rate lookups read C and prev_cnt as
+    // written above by other lanes: agent fence (L1 invalidate) + barrier
+    __threadfence();
+    __syncthreads();
+    if (uniform_int(sh.pass_done)) break;
     }
 }
 
@@ -1349,10 +1361,12 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
 
 using namespace gsc;
 
-// One batched KNNScanReduce pass for every frame (K = 2^logk, 256..4096,
-// D = 8 or 16).  Returns hipErrorInvalidValue for shapes it does not cover.
+// Batched KNNScanReduce for every frame (K = 2^logk, 256..4096, D = 8 or 16):
+// each frame runs its passes from frp->iters until it converges, reaches
+// max_passes or meets a NaN pass (left to the generic kernel).  Returns
+// hipErrorInvalidValue for shapes it does not cover.
 extern "C" hipError_t gsc_launch_scan_batch(int D, int logk, ReduceFrame* frames, int nframes, const float* X,
-                                            float* C, int* is, const float* rate_tab, double tol, int pass,
+                                            float* C, int* is, const float* rate_tab, double tol, int max_passes,
                                             hipStream_t st) {
     const int K = 1 << logk;
     const int threads = 64 * (K >= 512 ? K / 512 : 1);
@@ -1362,7 +1376,7 @@ extern "C" hipError_t gsc_launch_scan_batch(int D, int logk, ReduceFrame* frames
         (void)hipFuncSetAttribute((const void*)scan_batch_kernel<DV, LK>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                   (int)shm);                                                                           \
         hipLaunchKernelGGL((scan_batch_kernel<DV, LK>), dim3(nframes), dim3(threads), shm, st, frames, nframes, X, C,   \
-                           is, rate_tab, tol, pass);                                                                   \
+                           is, rate_tab, tol, max_passes);                                                                   \
         return hipGetLastError();                                                                                      \
     }
     SB(8, 8) SB(8, 9) SB(8, 10) SB(8, 11) SB(8, 12)
