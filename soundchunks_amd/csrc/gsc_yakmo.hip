@@ -1,6 +1,6 @@
 // yakmo k-means++ seeding + seeding means (yakmo_single.dll, called by
 // TFrame.Reduce at encoder.lpr:824-828 as yakmo_create(K,1,0,1,0,0,v)),
-// one workgroup (4 waves) per frame.  Restated from the DLL in SURVEY.md
+// one workgroup (9 waves) per frame.  Restated from the DLL in SURVEY.md
 // App. C.1 and oracle/yakmo_oracle.c; only the means of the seeding
 // assignment reach the .gsc.
 //
@@ -15,9 +15,9 @@
 // therefore the DLL's probe sequence even where tiny negative d make cum
 // non-monotone.
 //
-// Roles: wave 0 only picks and chains (the prefix is the critical path, one
-// dependent f32 add per point); waves 1..4 compute the distances of one
-// 256-point block per step, with the next block's loads issued a step ahead so
+// Roles: wave 0 only picks and chains (the prefix, an integer prefix sum per
+// binade where that is exact, see chain_step_binade); waves 1..8 compute the distances of one
+// 512-point block per step, with the next block's loads issued a step ahead so
 // HBM latency hides under the chain.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -31,7 +31,7 @@ __device__ __forceinline__ float fa(float a, float b) { return __fadd_rn(a, b); 
 __device__ __forceinline__ float fs(float a, float b) { return __fsub_rn(a, b); }
 __device__ __forceinline__ float fm(float a, float b) { return __fmul_rn(a, b); }
 
-constexpr int kYBlock = 256;          // points per pipeline step (waves 1..4)
+constexpr int kYBlock = 512;          // points per pipeline step (waves 1..8)
 constexpr int kYThreads = 64 + kYBlock;  // wave 0: picks + prefix chain
 constexpr int kYBits = 262144 / 32;   // chosen-point bitmap in LDS (N <= 262144)
 
@@ -52,6 +52,68 @@ __device__ __forceinline__ float cum_at(const float* __restrict__ d0, const floa
     const int last = m & 63;
     for (int l = 0; l <= last; ++l) run = fa(run, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)));
     return run;
+}
+
+// Inclusive wave64 prefix sum of 32-bit integers (wrap-around arithmetic).
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t x, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+
+// One 256-point step of the sequential f32 prefix cum[n] = fl(cum[n-1] + d[n])
+// without the dependent add chain, exact or not at all.
+//
+// While the running total stays in one binade [2^e, 2^(e+1)), every partial
+// sum is a multiple of u = 2^(e-23): run = m*u with m in [2^23, 2^24).  Then
+// fl(m*u + d) = (m + n)*u with n = round(d/u), *provided* m + d/u is not a
+// tie (the even choice would depend on m) and the exact sum m + d/u stays
+// inside (2^23, 2^24 - 1/2), which m + n in [2^23 + 1, 2^24 - 2] guarantees
+// (the sum stays in the binade, so its rounding grid is still u).  Under
+// those conditions the chain is an integer prefix sum: the d/u roundings are
+// independent of each other and of the order, and the integer sums are exact.
+// The step takes the fast path only when every point meets the conditions
+// (no tie, |d/u| < 2^24, every partial m + n_0 + ... + n_k in range);
+// otherwise it returns false and the caller adds the step point by point.
+// run must be a positive normal f32 (a zero or subnormal total has a
+// different grid).  Writes the four 64-point checkpoints and the new run.
+__device__ __forceinline__ bool chain_step_binade(const float* __restrict__ ring, float* __restrict__ ck, int lane,
+                                                  float* run_io) {
+    const float run = *run_io;
+    if (!(run >= 1.17549435e-38f)) return false;  // zero, negative, subnormal (or NaN)
+    const int fe = __builtin_amdgcn_frexp_expf(run);  // run = f * 2^fe, f in [0.5, 1)
+    const int sc = 24 - fe;                          // d/u = d * 2^sc
+    const uint32_t m0 = (uint32_t)__builtin_ldexpf(run, sc);  // in [2^23, 2^24), exact
+    uint32_t p[kYBlock / 64];
+    bool good = true;
+#pragma unroll
+    for (int k = 0; k < kYBlock / 64; ++k) {
+        const float t = __builtin_ldexpf(ring[k * 64 + lane], sc);  // exact unless |t| is far below 1/2
+        const bool ok = __builtin_fabsf(t) < 16777216.0f && (t - __builtin_floorf(t)) != 0.5f;  // NaN: not ok
+        good &= ok;
+        p[k] = (uint32_t)(int)(ok ? __builtin_rintf(t) : 0.0f);
+    }
+#pragma unroll
+    for (int k = 0; k < kYBlock / 64; ++k) p[k] = wave_incl_scan_u32(p[k], lane);
+    uint32_t off = m0;
+#pragma unroll
+    for (int k = 0; k < kYBlock / 64; ++k) {
+        const uint32_t v = off + p[k];
+        // m + partial in [2^23 + 1, 2^24 - 2]: then the exact sum, within 1/2 of
+        // it, lies strictly inside the binade and rounds on the grid u
+        good &= (v - 8388609u) < 8388606u;
+        off = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+        p[k] = off;  // the block's last partial: its checkpoint
+    }
+    if (__ballot(!good) != 0ull) return false;
+#pragma unroll
+    for (int k = 0; k < kYBlock / 64; ++k)
+        if (lane == 0) ck[k] = __builtin_ldexpf((float)p[k], -sc);  // exact: m < 2^24, same binade
+    *run_io = __builtin_ldexpf((float)off, -sc);
+    return true;
 }
 
 }  // namespace
@@ -135,6 +197,8 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
             for (int b = 0; b <= nblk; ++b) {
                 if (chain && b > 0) {
                     const int base = (b - 1) * kYBlock;
+                    if (base + kYBlock <= N && chain_step_binade(sh.ring[(b - 1) & 1], ckpt + (base >> 6), lane, &run))
+                        goto step_done;
 #pragma unroll
                     for (int k = 0; k < kYBlock / 64; ++k) {
                         const int cnt = min(64, N - (base + k * 64));
@@ -160,6 +224,7 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
                         if (cnt > 0 && lane == 0) ckpt[((base + k * 64) >> 6)] = run;
                     }
                 }
+            step_done:
                 __syncthreads();
             }
             total = run;

@@ -67,3 +67,35 @@ def test_gsc_matches_golden(name):
     got = sc.Encoder(argv).encode(make())
     assert len(got) == len(expected)
     assert got == expected
+
+
+def _yakmo_dataset(kind, n, d, seed):
+    rng = np.random.default_rng(seed)
+    if kind == "gauss":
+        return rng.standard_normal((n, d)).astype(np.float32) * 50.0
+    if kind == "integer":  # many equal distances and duplicate points (zero / tiny negative d)
+        return rng.integers(-3, 4, size=(n, d)).astype(np.float32)
+    if kind == "outliers":  # a few huge points: the prefix jumps across many binades at once
+        x = rng.standard_normal((n, d)).astype(np.float32)
+        x[rng.integers(0, n, size=n // 500)] *= 1e4
+        return x
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind,n,d,k", [("gauss", 5000, 16, 256), ("integer", 3000, 16, 512),
+                                        ("outliers", 7000, 8, 256), ("gauss", 20000, 16, 1024)])
+def test_yakmo_seed_means_synthetic(oracle, kind, n, d, k):
+    """The binade-exact prefix fast path (gsc_yakmo.hip) against the oracle's sequential f32 chain."""
+    import ctypes
+
+    import soundchunks_amd as sc
+
+    x = _yakmo_dataset(kind, n, d, 1234 + n)
+    want = np.zeros((k, d), dtype=np.float32)
+    labels = np.zeros(n, dtype=np.int32)
+    fp = ctypes.POINTER(ctypes.c_float)
+    rc = oracle.load().ora_yakmo_seed_means(n, d, x.ctypes.data_as(fp), k, want.ctypes.data_as(fp),
+                                            labels.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+    assert rc == 0
+    got = sc.yakmo_seed_means(x, k)
+    np.testing.assert_array_equal(_bits(got), _bits(want))
