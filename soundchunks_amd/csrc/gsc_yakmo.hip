@@ -17,7 +17,7 @@
 //
 // Roles: wave 0 only picks and chains (the prefix, an integer prefix sum per
 // binade where that is exact, see chain_step_binade); waves 1..8 compute the distances of one
-// 512-point block per step, with the next block's loads issued a step ahead so
+// 2048-point block per step (4 points per thread), with the next block's loads issued a step ahead so
 // HBM latency hides under the chain.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -31,15 +31,26 @@ __device__ __forceinline__ float fa(float a, float b) { return __fadd_rn(a, b); 
 __device__ __forceinline__ float fs(float a, float b) { return __fsub_rn(a, b); }
 __device__ __forceinline__ float fm(float a, float b) { return __fmul_rn(a, b); }
 
-constexpr int kYBlock = 512;          // points per pipeline step (waves 1..8)
-constexpr int kYThreads = 64 + kYBlock;  // wave 0: picks + prefix chain
+constexpr int kYDist = 512;            // distance threads (waves 1..8)
+constexpr int kYBlock = kYDist * 4;    // largest step (points): ring size
+// points per distance thread per step (loads in flight), bounded by the VGPR
+// budget of 9 waves (168): 4 rows of D = 8, 2 of D = 16, 1 of D = 32
+template <int D>
+constexpr int yakmo_per() {
+    return 1;
+}
+constexpr int kYThreads = 64 + kYDist;   // wave 0: picks + prefix chain
 constexpr int kYBits = 262144 / 32;   // chosen-point bitmap in LDS (N <= 262144)
 
 struct YakmoShared {
     alignas(16) float ring[2][kYBlock];    // d0 of the last two blocks (chain input)
     uint32_t chosen[kYBits];
-    int cursor[kMaxK];         // stable counting sort of the final assignment
+    union {
+        int cursor[kMaxK];     // stable counting sort of the final assignment
+        float sdlo[kMaxK];     // picks: lower bound of |c_i - c_a|^2 per earlier seed a
+    };
     float c[32];               // current seed
+    float cmax;                // max |c_a|^2 over the seeds so far
     int idx;
     float total;
 };
@@ -79,7 +90,8 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t x, int lane) {
 // (no tie, |d/u| < 2^24, every partial m + n_0 + ... + n_k in range);
 // otherwise it returns false and the caller adds the step point by point.
 // run must be a positive normal f32 (a zero or subnormal total has a
-// different grid).  Writes the four 64-point checkpoints and the new run.
+// different grid).  Writes the NB 64-point checkpoints and the new run.
+template <int NB>
 __device__ __forceinline__ bool chain_step_binade(const float* __restrict__ ring, float* __restrict__ ck, int lane,
                                                   float* run_io) {
     const float run = *run_io;
@@ -87,20 +99,20 @@ __device__ __forceinline__ bool chain_step_binade(const float* __restrict__ ring
     const int fe = __builtin_amdgcn_frexp_expf(run);  // run = f * 2^fe, f in [0.5, 1)
     const int sc = 24 - fe;                          // d/u = d * 2^sc
     const uint32_t m0 = (uint32_t)__builtin_ldexpf(run, sc);  // in [2^23, 2^24), exact
-    uint32_t p[kYBlock / 64];
+    uint32_t p[NB];
     bool good = true;
 #pragma unroll
-    for (int k = 0; k < kYBlock / 64; ++k) {
+    for (int k = 0; k < NB; ++k) {
         const float t = __builtin_ldexpf(ring[k * 64 + lane], sc);  // exact unless |t| is far below 1/2
         const bool ok = __builtin_fabsf(t) < 16777216.0f && (t - __builtin_floorf(t)) != 0.5f;  // NaN: not ok
         good &= ok;
         p[k] = (uint32_t)(int)(ok ? __builtin_rintf(t) : 0.0f);
     }
 #pragma unroll
-    for (int k = 0; k < kYBlock / 64; ++k) p[k] = wave_incl_scan_u32(p[k], lane);
+    for (int k = 0; k < NB; ++k) p[k] = wave_incl_scan_u32(p[k], lane);
     uint32_t off = m0;
 #pragma unroll
-    for (int k = 0; k < kYBlock / 64; ++k) {
+    for (int k = 0; k < NB; ++k) {
         const uint32_t v = off + p[k];
         // m + partial in [2^23 + 1, 2^24 - 2]: then the exact sum, within 1/2 of
         // it, lies strictly inside the binade and rounds on the grid u
@@ -110,7 +122,7 @@ __device__ __forceinline__ bool chain_step_binade(const float* __restrict__ ring
     }
     if (__ballot(!good) != 0ull) return false;
 #pragma unroll
-    for (int k = 0; k < kYBlock / 64; ++k)
+    for (int k = 0; k < NB; ++k)
         if (lane == 0) ck[k] = __builtin_ldexpf((float)p[k], -sc);  // exact: m < 2^24, same binade
     *run_io = __builtin_ldexpf((float)off, -sc);
     return true;
@@ -149,7 +161,9 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
 
     uint64_t rx = 123456789ull, ry = 362436069ull, rz = 521288629ull, rw = 88675123ull;
     float total = 0.0f;
-    const int nblk = (N + kYBlock - 1) / kYBlock;
+    constexpr int kYPer = yakmo_per<D>();
+    constexpr int BLK = kYDist * kYPer;  // points per pipeline step
+    const int nblk = (N + BLK - 1) / BLK;
     const int dt = tid - 64;  // distance thread of waves 1..4 (negative on wave 0)
     for (int i = 0; i < K; ++i) {
         // ---- pick (wave 0; the RNG runs redundantly in every thread)
@@ -186,27 +200,36 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
             if (lane == 0) {
                 sh.chosen[idx >> 5] |= 1u << (idx & 31);
                 sh.idx = (int)idx;
+                sh.cmax = i == 0 ? norm[idx] : fmaxf(sh.cmax, norm[idx]);
             }
-            if (lane < D) sh.c[lane] = X[(int64_t)idx * D + lane];
+            if (lane < D) {
+                const float v = X[(int64_t)idx * D + lane];
+                sh.c[lane] = v;
+                C[(int64_t)i * D + lane] = v;  // the seeds (C is overwritten by the means at the end)
+            }
         }
         __syncthreads();
         const bool chain = i < K - 1;
         if (wave == 0) {
+            __syncthreads();  // the distance waves' seed-distance table
             // sequential f32 prefix over the blocks as they complete (encoder's cum[], DLL @0x180001e74)
             float run = 0.0f;
             for (int b = 0; b <= nblk; ++b) {
                 if (chain && b > 0) {
-                    const int base = (b - 1) * kYBlock;
-                    if (base + kYBlock <= N && chain_step_binade(sh.ring[(b - 1) & 1], ckpt + (base >> 6), lane, &run))
-                        goto step_done;
-#pragma unroll
-                    for (int k = 0; k < kYBlock / 64; ++k) {
+                    const int base = (b - 1) * BLK;
+                    const float* rg = sh.ring[(b - 1) & 1];
+                    if (base + BLK <= N && chain_step_binade<BLK / 64>(rg, ckpt + (base >> 6), lane, &run)) {
+                        __syncthreads();
+                        continue;
+                    }
+                    for (int k = 0; k < BLK / 64; ++k) {
                         const int cnt = min(64, N - (base + k * 64));
+                        if (cnt <= 0) break;
                         if (cnt == 64) {
                             // the 64 values as LDS broadcast reads into VGPRs (every lane loads
                             // the same row), then the dependent adds back to back: no VALU
                             // readlane per point on the critical chain
-                            const float4* row = reinterpret_cast<const float4*>(&sh.ring[(b - 1) & 1][k * 64]);
+                            const float4* row = reinterpret_cast<const float4*>(&rg[k * 64]);
                             float4 sv[16];
 #pragma unroll
                             for (int l = 0; l < 16; ++l) sv[l] = row[l];
@@ -218,13 +241,12 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
                                 run = fa(run, sv[l].w);
                             }
                         } else {
-                            const int v = __float_as_int(sh.ring[(b - 1) & 1][k * 64 + lane]);
+                            const int v = __float_as_int(rg[k * 64 + lane]);
                             for (int l = 0; l < cnt; ++l) run = fa(run, __int_as_float(__builtin_amdgcn_readlane(v, l)));
                         }
-                        if (cnt > 0 && lane == 0) ckpt[((base + k * 64) >> 6)] = run;
+                        if (lane == 0) ckpt[((base + k * 64) >> 6)] = run;
                     }
                 }
-            step_done:
                 __syncthreads();
             }
             total = run;
@@ -233,35 +255,98 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
 #pragma unroll
             for (int j = 0; j < D; ++j) c[j] = sh.c[j];
             const float cn = norm[sh.idx];
-            // one pass over the points: d0/id update, block b+1 prefetched during step b
-            float xv[D];
-            float xn = 0.0f, dold = 0.0f;
-            if (dt < N) {
+            const float cmax = sh.cmax;
+            // Seed-distance table: sdlo[a] <= |c_i - c_a|^2 (the f32 sum of squared
+            // differences, lowered by 2^-16 relative to cover its rounding).
+            for (int a = dt; a < i; a += kYDist) {
+                float s2 = 0.0f;
 #pragma unroll
-                for (int j = 0; j < D; ++j) xv[j] = X[(int64_t)dt * D + j];
-                xn = norm[dt];
-                dold = d0[dt];
+                for (int j = 0; j < D; ++j) {
+                    const float t = fs(C[(int64_t)a * D + j], c[j]);
+                    s2 = fa(s2, fm(t, t));
+                }
+                sh.sdlo[a] = fm(s2, 0.99998474f);
+            }
+            __syncthreads();
+            // Elkan skip: with E = (|x|^2 + cmax) 2^-16 >= the rounding error of any of the
+            // DLL's expanded-form distances from x (< 80 u (|x|^2 + |c|^2)), the computed
+            // d0 = d(x, c_a) and d(x, c_i) are within E of the true squares, so
+            // |c_i - c_a| >= 2 sqrt(max(d0, 0) + E) implies d(x, c_i) >= d0: no strict
+            // improvement, and the point's X row need not be read for this pick.
+            auto skip_of = [&](float dold, float xn, int a) -> bool {
+                if (i == 0) return false;
+                const float e = fm(fa(xn, cmax), 1.52587891e-05f);
+                const float need = fm(fm(fa(fmaxf(dold, 0.0f), e), 4.0f), 1.00000381f);
+                return sh.sdlo[a] >= need;
+            };
+            // one pass over the points: d0/id update; block b+1's X rows (when not
+            // skipped) and block b+2's d0/|x|^2/id are loaded during step b.  Each
+            // thread owns kYPer points per block (kYDist apart, coalesced).
+            float xv[kYPer][D];
+            float xn[kYPer], dold[kYPer], xn_n[kYPer], dold_n[kYPer];
+            bool skip[kYPer];
+            int a_n[kYPer];
+#pragma unroll
+            for (int q = 0; q < kYPer; ++q) {
+                const int n0 = q * kYDist + dt, n1 = n0 + BLK;
+                xn[q] = 0.0f;
+                dold[q] = 0.0f;
+                skip[q] = true;
+                if (n0 < N) {
+                    xn[q] = norm[n0];
+                    dold[q] = d0[n0];
+                    skip[q] = skip_of(dold[q], xn[q], i == 0 ? 0 : idv[n0]);
+                    if (!skip[q]) {
+#pragma unroll
+                        for (int j = 0; j < D; ++j) xv[q][j] = X[(int64_t)n0 * D + j];
+                    }
+                }
+                xn_n[q] = 0.0f;
+                dold_n[q] = 0.0f;
+                a_n[q] = 0;
+                if (n1 < N) {
+                    xn_n[q] = norm[n1];
+                    dold_n[q] = d0[n1];
+                    a_n[q] = i == 0 ? 0 : idv[n1];
+                }
             }
             for (int b = 0; b <= nblk; ++b) {
-                const int n = b * kYBlock + dt;
-                if (b < nblk && n < N) {
-                    float d = fa(fa(cn, xn), 0.0f);
 #pragma unroll
-                    for (int j = 0; j < D; ++j) d = fs(d, fm(fa(xv[j], xv[j]), c[j]));
-                    float dn = dold;
-                    if (i == 0 || dn > d) {
-                        dn = d;
-                        d0[n] = d;
-                        idv[n] = i;
+                for (int q = 0; q < kYPer; ++q) {
+                    const int n = b * BLK + q * kYDist + dt;
+                    if (b < nblk && n < N) {
+                        float dn = dold[q];
+                        if (!skip[q]) {
+                            float d = fa(fa(cn, xn[q]), 0.0f);
+#pragma unroll
+                            for (int j = 0; j < D; ++j) d = fs(d, fm(fa(xv[q][j], xv[q][j]), c[j]));
+                            if (i == 0 || dn > d) {
+                                dn = d;
+                                d0[n] = d;
+                                idv[n] = i;
+                            }
+                        }
+                        sh.ring[b & 1][q * kYDist + dt] = dn;
                     }
-                    sh.ring[b & 1][dt] = dn;
                 }
-                const int n2 = n + kYBlock;
-                if (b + 1 < nblk && n2 < N) {
 #pragma unroll
-                    for (int j = 0; j < D; ++j) xv[j] = X[(int64_t)n2 * D + j];
-                    xn = norm[n2];
-                    dold = d0[n2];
+                for (int q = 0; q < kYPer; ++q) {
+                    const int n2 = (b + 1) * BLK + q * kYDist + dt;
+                    if (b + 1 < nblk && n2 < N) {
+                        xn[q] = xn_n[q];
+                        dold[q] = dold_n[q];
+                        skip[q] = skip_of(dold[q], xn[q], a_n[q]);
+                        if (!skip[q]) {
+#pragma unroll
+                            for (int j = 0; j < D; ++j) xv[q][j] = X[(int64_t)n2 * D + j];
+                        }
+                        const int n3 = n2 + BLK;
+                        if (b + 2 < nblk && n3 < N) {
+                            xn_n[q] = norm[n3];
+                            dold_n[q] = d0[n3];
+                            a_n[q] = i == 0 ? 0 : idv[n3];
+                        }
+                    }
                 }
                 __syncthreads();
             }
