@@ -412,12 +412,25 @@ __device__ __forceinline__ void knn_chunk_dists(const float (&q)[CS], const floa
     }
 }
 
+// Bound-then-exact: the expanded form |q|^2 + |v|^2 -+ 2 q.v (fma dot
+// products; one dot serves a candidate and its negation) is within
+// eps_b = (|q|^2 + vmax) 2^-17 of the exact sequential distance (error budget:
+// fma dot <= CS u (|q|^2 + |v|^2)/2 x 2, norms <= CS u each, two adds, the
+// exact sum <= (CS + 1) u x 2 (|q|^2 + |v|^2): < 90 u for CS <= 16, against
+// 128 u).  The exact distances are computed only where the bounds cannot decide:
+// pass 1 evaluates a candidate exactly only while its bound is within 2 eps_b of
+// the running minimum bound (the exact minimum always is, as the threshold only
+// falls); pass 2 only where some variant's bound may reach the acceptance
+// threshold, which is monotone in e, so skipped variants cannot qualify.  The
+// chosen index and the tie count are those of the all-exact scan.
 template <int CS>
 __global__ __launch_bounds__(256) void knnfit_kernel(FitFrame* __restrict__ frames, int nframes,
                                                       const float* __restrict__ cand_all, const float* __restrict__ q_all,
                                                       int* __restrict__ out_all, int tiles_per_frame, int tile_r) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float* tile = reinterpret_cast<float*>(smem);
+    float* vvt = tile + (size_t)tile_r * CS;  // |v|^2 per candidate of the tile
+    __shared__ unsigned int s_vmax;
     const int fi = blockIdx.x / tiles_per_frame;
     const int ti = blockIdx.x - fi * tiles_per_frame;
     if (fi >= nframes) return;
@@ -431,8 +444,26 @@ __global__ __launch_bounds__(256) void knnfit_kernel(FitFrame* __restrict__ fram
     float q[CS];
 #pragma unroll
     for (int j = 0; j < CS; ++j) q[j] = active ? q_all[fr->q_off + (int64_t)qi * CS + j] : 0.0f;
-    float e0 = __builtin_inff();
-    float s0 = 0.0f;
+    // vmax >= |v|^2 over the frame's candidates (nonnegative floats order as their bits)
+    if (threadIdx.x == 0) s_vmax = 0u;
+    __syncthreads();
+    {
+        unsigned int m = 0u;
+        for (int c = threadIdx.x; c < R; c += 256) {
+            float vv = 0.0f;
+#pragma unroll
+            for (int j = 0; j < CS; ++j) vv = __fmaf_rn(cand[(int64_t)c * CS + j], cand[(int64_t)c * CS + j], vv);
+            m = max(m, __float_as_uint(vv * 1.0000153f));  // NaN bits exceed +inf: eb = NaN, nothing is skipped
+        }
+        atomicMax(&s_vmax, m);
+    }
+    float qq = 0.0f;
+#pragma unroll
+    for (int j = 0; j < CS; ++j) qq = __fmaf_rn(q[j], q[j], qq);
+    __syncthreads();
+    const float eb = (qq + __uint_as_float(s_vmax)) * 7.62939453e-06f;  // 2^-17
+    float e0 = __builtin_inff(), mt = __builtin_inff();
+    float s0 = 0.0f, ehi = 0.0f;
     int best = -1, cnt = 0;
     for (int pass = 0; pass < 2; ++pass) {
         for (int c0 = 0; c0 < R; c0 += tile_r) {
@@ -440,13 +471,34 @@ __global__ __launch_bounds__(256) void knnfit_kernel(FitFrame* __restrict__ fram
             __syncthreads();
             for (int k = threadIdx.x; k < nr * CS; k += 256) tile[k] = cand[(int64_t)c0 * CS + k];
             __syncthreads();
-            for (int c = 0; c < nr; ++c) {
-                float e[4];
-                knn_chunk_dists<CS>(q, tile + c * CS, e);
-                if (pass == 0) {
+            for (int c = threadIdx.x; c < nr; c += 256) {
+                float vv = 0.0f;
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) e0 = (e[k] < e0) ? e[k] : e0;
-                } else {
+                for (int j = 0; j < CS; ++j) vv = __fmaf_rn(tile[c * CS + j], tile[c * CS + j], vv);
+                vvt[c] = vv;
+            }
+            __syncthreads();
+            for (int c = 0; c < nr; ++c) {
+                const float* v = tile + c * CS;
+                float df = 0.0f, dr = 0.0f;
+#pragma unroll
+                for (int j = 0; j < CS; ++j) {
+                    df = __fmaf_rn(q[j], v[j], df);
+                    dr = __fmaf_rn(q[j], v[CS - 1 - j], dr);
+                }
+                const float base = qq + vvt[c];
+                const float mn = base - 2.0f * fmaxf(fabsf(df), fabsf(dr));  // min over the 4 variants
+                if (pass == 0) {
+                    mt = fminf(mt, mn);
+                    if (!(mn > mt + 2.0f * eb)) {  // (a NaN bound evaluates exactly)
+                        float e[4];
+                        knn_chunk_dists<CS>(q, v, e);
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) e0 = (e[k] < e0) ? e[k] : e0;
+                    }
+                } else if (!(mn - eb > ehi)) {
+                    float e[4];
+                    knn_chunk_dists<CS>(q, v, e);
                     // f order: 4c+0 fwd, 4c+1 rev, 4c+2 neg fwd, 4c+3 neg rev
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
@@ -460,7 +512,12 @@ __global__ __launch_bounds__(256) void knnfit_kernel(FitFrame* __restrict__ fram
                 }
             }
         }
-        if (pass == 0) s0 = __fsqrt_rn(e0 / (float)CS);
+        if (pass == 0) {
+            s0 = __fsqrt_rn(e0 / (float)CS);
+            // acceptance is monotone in e: e > CS (s0 + eps)^2 (1 + 2^-16) never qualifies
+            const float t = s0 + eps;
+            ehi = (float)CS * t * t * 1.0000153f;
+        }
     }
     if (active) {
         out_all[fr->out_off + qi] = (cnt > 64) ? -1 : best;
@@ -499,10 +556,11 @@ extern "C" hipError_t gsc_launch_knnfit(int CS, FitFrame* frames, int nframes, i
                                         const float* cand, const float* q, int* out, hipStream_t st) {
     const int tiles = (max_n + 255) / 256;
     dim3 grid(nframes * tiles), block(256);
-    int tile_r = (128 * 1024) / (CS * (int)sizeof(float));
+    // 72 KB tiles (values + |v|^2): two workgroups per CU
+    int tile_r = (72 * 1024) / ((CS + 1) * (int)sizeof(float));
     if (tile_r > max_r) tile_r = max_r;
     if (tile_r < 1) tile_r = 1;
-    size_t shm = (size_t)tile_r * CS * sizeof(float);
+    size_t shm = (size_t)tile_r * (CS + 1) * sizeof(float);
     switch (CS) {
 #define KF(CSV)                                                                                                   \
     case CSV:                                                                                                     \
