@@ -99,3 +99,32 @@ def test_yakmo_seed_means_synthetic(oracle, kind, n, d, k):
     assert rc == 0
     got = sc.yakmo_seed_means(x, k)
     np.testing.assert_array_equal(_bits(got), _bits(want))
+
+
+@pytest.mark.parametrize("cs,r,n,eps,seed", [(8, 600, 3000, 0.0026, 1), (8, 4096, 2000, 1.0 / 32767, 2),
+                                             (4, 300, 2500, 0.01, 3), (16, 1000, 1500, 0.004, 4)])
+def test_knnfit_synthetic_ties(oracle, cs, r, n, eps, seed):
+    """Bound-then-exact KNNFit (gsc_kernels.hip) vs the oracle's ANN 64-NN + tie rule on
+    8-bit-quantised candidates with duplicates and queries on / near the candidates."""
+    import ctypes
+
+    import soundchunks_amd as sc
+
+    rng = np.random.default_rng(seed)
+    base = np.round(rng.uniform(-1, 1, size=(r // 2, cs)) * 127) / 127
+    fwd = np.concatenate([base, base[rng.integers(0, len(base), size=r - len(base))]]).astype(np.float32)
+    rng.shuffle(fwd)
+    pick = fwd[rng.integers(0, r, size=n)]
+    flip = rng.integers(0, 4, size=n)  # queries near every variant: fwd, rev, neg, neg rev
+    pick = np.where((flip & 1)[:, None] == 1, pick[:, ::-1], pick) * np.where(flip >= 2, -1.0, 1.0)[:, None]
+    noise = rng.normal(0, 0.002, size=pick.shape) * (rng.uniform(size=(n, 1)) < 0.7)
+    q = (pick + noise).astype(np.float32)
+    cand4 = np.empty((4 * r, cs), dtype=np.float32)
+    cand4[0::4], cand4[1::4], cand4[2::4], cand4[3::4] = fwd, fwd[:, ::-1], -fwd, -fwd[:, ::-1]
+    want = np.zeros(n, dtype=np.int32)
+    fp = ctypes.POINTER(ctypes.c_float)
+    oracle.load().ora_knnfit_assign(4 * r, cs, np.ascontiguousarray(cand4).ctypes.data_as(fp), n,
+                                    q.ctypes.data_as(fp), ctypes.c_float(eps),
+                                    want.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+    got = sc.knnfit_assign(fwd, q, eps)
+    np.testing.assert_array_equal(got, want)
