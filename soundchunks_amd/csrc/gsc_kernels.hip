@@ -564,7 +564,9 @@ extern "C" hipError_t gsc_launch_knnfit(int CS, FitFrame* frames, int nframes, i
     switch (CS) {
 #define KF(CSV)                                                                                                   \
     case CSV:                                                                                                     \
-        hipFuncSetAttribute((const void*)knnfit_kernel<CSV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm); \
+        if (hipError_t e = hipFuncSetAttribute((const void*)knnfit_kernel<CSV>,                                   \
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm))             \
+            return e;                                                                                             \
         hipLaunchKernelGGL(knnfit_kernel<CSV>, grid, block, shm, st, frames, nframes, cand, q, out, tiles, tile_r);          \
         break;
         KF(4)
