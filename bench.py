@@ -1,13 +1,16 @@
 """bench.py -- SoundChunks encode throughput on MI355X (driver contract).
 
 Metric (BASELINE.json): encoded Msamples/s @44.1 kHz stereo, ChunkSize=8,
-ChunkCount=4096 (configs[1]), bit-exact .gsc.  One step = one full encode of
-this rank's share of a synthetic 44.1 kHz stereo signal (SURVEY.md §8d:
-0.25 sin(440/660 Hz) + 0.05 N(0,1), PCG64(20250217)): host pre-pass, per-frame
-DSP, GPU Reduce (yakmo + KNNScanReduce) and KNNFit, bit packing.  Frames are
-independent: with N GPUs each rank encodes a contiguous frame range of an
-N-times longer signal (weak scaling) and rank 0 gathers the per-frame .gsc
-bytes (torch.distributed over RCCL/xGMI).
+ChunkCount=4096 (configs[1]), bit-exact .gsc.  The job's one-off host pass
+(Load + PrepareFrames: the sequential frame-boundary scan of the whole file,
+encoder.lpr:1294-1429) runs once before timing and is reported as prepare_ms.
+One step = one encode of this rank's frames of a synthetic 44.1 kHz stereo
+signal (0.25 sin(440/660 Hz) + 0.05 N(0,1), PCG64(20250217)):
+per-frame sample staging and DSP, GPU Reduce (yakmo + KNNScanReduce) and
+KNNFit, bit packing.  Frames are independent: with N GPUs each rank encodes a
+contiguous frame range (balanced by chunk count) of an N-times longer signal
+(weak scaling) and rank 0 gathers the per-frame .gsc bytes (torch.distributed
+over RCCL/xGMI).
 
 python bench.py [--gpus N] [--steps K] [--warmup W] [--seconds S] [--config c2|c3|c1]
 """
@@ -40,20 +43,65 @@ def _dist_env():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def cpu_baseline(argv, seconds: float, rate: int, channels: int) -> dict:
-    """Oracle (C restatement, 1 thread) on a bounded sample of the same signal."""
+def _cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(argv, rate: int, channels: int, frame_seconds: float, threads: int, runs: int = 3) -> dict:
+    """SURVEY.md §8d CPU baseline: the oracle (C restatement of the reference
+    encoder, oracle/), frame-parallel like the reference's MTProcs pool
+    (encoder.lpr:1449).  Single thread: `runs` independent 1-thread encodes of
+    one full frame, run side by side on separate cores (ctypes releases the
+    GIL), median.  All-core: `threads` threads on `threads` full frames of the
+    same signal and flags, one run (a full frame takes ~1.5 min on one core, so
+    three all-core runs would triple the bench's wall time)."""
+    import statistics
+    import threading
+
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_ffi  # the checker / CPU baseline, never the product path
     from soundchunks_amd.synth import synth_wav
 
-    wav = synth_wav(seconds, rate, channels)
-    t = time.time()
-    oracle_ffi.encode(wav, argv, threads=1)
-    dt = time.time() - t
-    samples = int(round(seconds * rate)) * channels
-    return {"value": round(samples / dt / 1e6, 6), "unit": "Msamples/s", "cores": 1, "kind": "port",
-            "sample": f"{seconds:g} s of the same synthetic {rate} Hz {channels}-ch signal and flags, "
-                      f"oracle/ C restatement on 1 host thread, {dt:.1f} s wall"}
+    oracle_ffi.load()
+    one_wav = synth_wav(frame_seconds, rate, channels)
+    one_samples = int(round(frame_seconds * rate)) * channels
+    walls = [0.0] * runs
+
+    def run(i):
+        t = time.perf_counter()
+        oracle_ffi.encode(one_wav, argv, threads=1)
+        walls[i] = time.perf_counter() - t
+
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(runs)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    w1 = statistics.median(walls)
+    many = frame_seconds * threads
+    wav = synth_wav(many, rate, channels)
+    t = time.perf_counter()
+    oracle_ffi.encode(wav, argv, threads=threads)
+    wn = time.perf_counter() - t
+    allv = int(round(many * rate)) * channels / wn / 1e6
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count()
+    return {"value": round(allv, 6), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"all-core: {threads} full {frame_seconds:g}-s frames ({many:g} s) of the same synthetic "
+                      f"{rate} Hz {channels}-ch signal and flags, oracle/ C restatement frame-parallel on {threads} "
+                      f"threads, 1 run ({wn:.1f} s); single-thread: one full frame, median of {runs} side-by-side runs",
+            "single_thread": {"value": round(one_samples / w1 / 1e6, 6), "cores": 1, "wall_s": round(w1, 2),
+                              "runs_s": [round(w, 2) for w in walls], "seconds_of_audio": frame_seconds},
+            "all_core": {"value": round(allv, 6), "cores": threads, "wall_s": round(wn, 2), "seconds_of_audio": many},
+            "cpu_model": _cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": share}
 
 
 def main():
@@ -64,8 +112,8 @@ def main():
     ap.add_argument("--seconds", type=float, default=1024.0,
                     help="audio seconds per GPU (1024 s = 256 frames of 4 s: one frame per CU)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--cpu-seconds", type=float, default=1.5,
-                    help="oracle baseline sample: 1.5 s = one 16.5k-chunk frame at the same flags, ~25 s of CPU")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="all-core CPU baseline threads (the GPU box's CPU share is 16 per GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -79,7 +127,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
     import soundchunks_amd as sc
-    from soundchunks_amd.shard import frame_range, gather_streams
+    from soundchunks_amd.shard import frame_range_weighted, gather_streams
     from soundchunks_amd.synth import synth_wav
 
     if ws > 1:
@@ -89,11 +137,15 @@ def main():
     total_seconds = args.seconds * ws
     wav = synth_wav(total_seconds, rate, ch)
     enc = sc.Encoder(argv)
-    nframes = enc.frame_count(wav)
-    b, e = frame_range(nframes, rank, ws)
+    # Load + PrepareFrames once per job (the sequential frame-boundary scan of
+    # the whole file, encoder.lpr:1294-1429); each step encodes this rank's
+    # frame range, balanced by chunk count (SURVEY.md §8e LPT)
+    prep = enc.prepare(wav)
+    nframes = prep.frame_count
+    b, e = frame_range_weighted(prep.frame_chunks().tolist(), rank, ws)
 
     def step():
-        out = enc.encode(wav, b, e)
+        out = prep.encode(b, e)
         if dist is not None:  # frame-ordered .gsc on rank 0: one padded all-gather (RCCL over xGMI)
             out = gather_streams(out, device=torch.device("cuda", local))
         return out
@@ -152,7 +204,8 @@ def main():
         "dtype": "f32",
         "data": f"synthetic (SURVEY.md §8d tone+noise, PCG64 20250217), {args.seconds:g} s per GPU",
         "config": {"workload": f"{desc}, {total_seconds:g} s synthetic", "frames": nframes, "argv": argv,
-                   "parallelism": f"frame-sharded x{ws}"},
+                   "parallelism": f"frame-sharded x{ws}", "rank0_frames": [b, e]},
+        "prepare_ms": round(prep.prepare_ms, 1),
         "realtime_x": round(value / (rate * ch / 1e6), 2),
         "roofline": {"bound": "valu", "kernel": "scan_batch_kernel", "achieved": round(achieved, 4),
                      "peak": VALU_F32_PEAK_TOPS, "unit": "Tops/s (algorithmic: the reference's sub+mul+add per leaf coordinate, 6K ops per sample per "
@@ -169,7 +222,7 @@ def main():
                  "solo_resolutions": tm["scan_restarts"]},
     }
     if not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(argv, args.cpu_seconds, rate, ch)
+        result["cpu_baseline"] = cpu_baseline(argv, rate, ch, enc.frame_length / 1000.0, args.cpu_threads)
     print(json.dumps(result))
     if dist is not None:
         dist.destroy_process_group()

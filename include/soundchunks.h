@@ -97,6 +97,20 @@ int gsc_encode_wav_frames(const uint8_t *wav, size_t wav_len, const gsc_options 
                           uint8_t **out, size_t *out_len, int *frame_count);
 int gsc_count_frames(const uint8_t *wav, size_t wav_len, const gsc_options *o, int *frame_count);
 
+/* Prepared WAV: TEncoder.Load + PrepareFrames (encoder.lpr:1111-1152,
+ * 1294-1429) run once per job; the frame boundaries of the whole file are then
+ * shared by every frame-range encode of that job (one rank per GPU encodes its
+ * range without rescanning the file).  gsc_prepare returns NULL on failure
+ * (gsc_last_error).  gsc_prepared_frame_chunks writes the chunkRefs count
+ * (chunks x channels) of every frame: the weights of the LPT frame sharding. */
+typedef struct gsc_prepared gsc_prepared;
+gsc_prepared *gsc_prepare(const uint8_t *wav, size_t wav_len, const gsc_options *o);
+int gsc_prepared_frame_count(const gsc_prepared *p);
+int gsc_prepared_frame_chunks(const gsc_prepared *p, int *chunks);
+int gsc_encode_prepared(gsc_prepared *p, int frame_begin, int frame_end, uint8_t **out, size_t *out_len);
+double gsc_prepared_prepare_ms(const gsc_prepared *p);
+void gsc_prepared_free(gsc_prepared *p);
+
 /* Device DSP of one frame (FindAttenuationDivider, encoder.lpr:566-605, and the
  * MakeChunks features, encoder.lpr:467-485): *feat = n_chunks x 2*ChunkSize
  * floats, allocated by the library (gsc_free).  Parity tests. */

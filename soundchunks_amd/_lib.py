@@ -84,6 +84,13 @@ SIGNATURES = {
                                              ctypes.c_int, ctypes.POINTER(_U8P), ctypes.POINTER(ctypes.c_size_t),
                                              _IP]),
     "gsc_count_frames": (ctypes.c_int, [_U8P, ctypes.c_size_t, ctypes.POINTER(GscOptions), _IP]),
+    "gsc_prepare": (ctypes.c_void_p, [_U8P, ctypes.c_size_t, ctypes.POINTER(GscOptions)]),
+    "gsc_prepared_frame_count": (ctypes.c_int, [ctypes.c_void_p]),
+    "gsc_prepared_frame_chunks": (ctypes.c_int, [ctypes.c_void_p, _IP]),
+    "gsc_encode_prepared": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_U8P),
+                                           ctypes.POINTER(ctypes.c_size_t)]),
+    "gsc_prepared_prepare_ms": (ctypes.c_double, [ctypes.c_void_p]),
+    "gsc_prepared_free": (None, [ctypes.c_void_p]),
     "gsc_frame_dsp": (ctypes.c_int, [_U8P, ctypes.c_size_t, ctypes.POINTER(GscOptions), ctypes.c_int, _IP,
                                      ctypes.POINTER(_FP), _IP]),
     "gsc_yakmo_seed_means": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _FP, ctypes.c_int, _FP]),

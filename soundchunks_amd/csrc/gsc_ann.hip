@@ -2,26 +2,20 @@
 // (ann_kdtree_create / _search / _pri_search / _search_multi /
 // _pri_search_multi).  The encoder itself uses the batched kernels in
 // gsc_kernels.hip; this file serves the per-query drop-in ABI, so it favours
-// exactness over speed: one lane runs ANN 1.1's sequential build and search
-// code (ANN.dll @0x180014620 ctor, @0x1800124b0 annkSearch,
-// @0x180011da0 annkPriSearch) on device memory.
+// exactness over speed: one lane runs ANN 1.1's sequential build (ANN.dll
+// @0x180014620 ctor); a search computes every live point distance with all
+// lanes of one workgroup and then walks ANN's DFS (@0x1800124b0 annkSearch)
+// or best-bin-first search (@0x180011da0 annkPriSearch) on one lane.
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <stdint.h>
 
+#include "gsc_device.h"
+
 namespace gsc {
 namespace ann {
 
-struct Tree {
-    const float* pts;  // n * dd, row major (the live point values)
-    int n, dd;
-    int* pidx;         // n
-    int* cd;           // heap-indexed split data, 2 * pow2ceil(n) entries
-    float* cv;
-    float* lo;
-    float* hi;
-    float* bnd;        // 2 * dd: bounding rect lo | hi
-};
+using Tree = gsc::AnnTree;
 
 __device__ __forceinline__ float fa(float a, float b) { return __fadd_rn(a, b); }
 __device__ __forceinline__ float fs(float a, float b) { return __fsub_rn(a, b); }
@@ -62,8 +56,7 @@ __device__ void median_split(const Tree& t, int* pidx, int n, int d, float* cv, 
 
 // ANNkd_tree ctor with ANN_KD_STD, bs = 1: annEnclRect, then rkd_tree with
 // kd_split (annMaxSpread + annMedianSplit) -- iterative pre-order
-__global__ void build_kernel(Tree t) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__device__ void build_seq(const Tree& t) {
     const int n = t.n, dd = t.dd;
     for (int i = 0; i < n; ++i) t.pidx[i] = i;
     int* pidx = t.pidx;
@@ -127,6 +120,17 @@ __global__ void build_kernel(Tree t) {
 }
 #undef PA
 
+__global__ void build_kernel(Tree t) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    build_seq(t);
+}
+
+// one tree per block (lane 0): the KNNFit candidate trees of several frames
+__global__ void build_many_kernel(const Tree* __restrict__ trees) {
+    if (threadIdx.x != 0) return;
+    build_seq(trees[blockIdx.x]);
+}
+
 struct MinK {
     float* key;
     int* info;
@@ -153,22 +157,48 @@ __device__ float box_dist(const float* q, const float* lo, const float* hi, int 
     return dist;
 }
 
-__device__ void leaf_visit(const Tree& t, const float* q, int p, MinK& mk) {
+// ANNkd_leaf::ann_search: dist = dist + (q[d] - p[d])^2 with the early exit
+// "some partial sum > min_dist" => not inserted.  The partial sums of
+// non-negative terms only grow, so on the precomputed full distance that test
+// is "dist > min_dist" -- except when the sum turns NaN, where the partial
+// sums are replayed.
+__device__ void leaf_visit(const Tree& t, const float* q, const float* __restrict__ dist, int p, MinK& mk) {
     const float min_dist = mk.max_key();
-    const float* pp = t.pts + (int64_t)t.pidx[p] * t.dd;
-    float dist = 0.0f;
-    int d;
-    for (d = 0; d < t.dd; ++d) {
-        const float tt = fs(q[d], pp[d]);
-        if ((dist = fa(dist, fm(tt, tt))) > min_dist) break;
+    const int pi = t.pidx[p];
+    const float dd = dist[pi];
+    bool exits;
+    if (dd == dd) {
+        exits = dd > min_dist;
+    } else {
+        const float* pp = t.pts + (int64_t)pi * t.dd;
+        float s = 0.0f;
+        exits = false;
+        for (int d = 0; d < t.dd && !exits; ++d) {
+            const float tt = fs(q[d], pp[d]);
+            s = fa(s, fm(tt, tt));
+            exits = s > min_dist;
+        }
     }
-    if (d >= t.dd) mk.insert(dist, t.pidx[p]);
+    if (!exits) mk.insert(dd, pi);
 }
 
 // mode 0: annkSearch (DFS); mode 1: annkPriSearch (best-bin-first)
+// All lanes compute the live distance of every point (sequential f32 over
+// d = 0..dd-1, the leaf's own order); lane 0 then walks ANN's search over the
+// stale tree with those distances.
 __global__ void query_kernel(Tree t, const float* __restrict__ q, int k, int mode, float eps, int* idxs, float* errs,
-                             float* mk_key, int* mk_info, float* pq_key, int* pq_h, int* pq_s, int* pq_n) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+                             float* dist, float* mk_key, int* mk_info, float* pq_key, int* pq_h, int* pq_s, int* pq_n) {
+    for (int i = threadIdx.x; i < t.n; i += blockDim.x) {
+        const float* pp = t.pts + (int64_t)i * t.dd;
+        float s = 0.0f;
+        for (int d = 0; d < t.dd; ++d) {
+            const float tt = fs(q[d], pp[d]);
+            s = fa(s, fm(tt, tt));
+        }
+        dist[i] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
     MinK mk{mk_key, mk_info, k, 0};
     const double max_err = (1.0 + (double)eps) * (1.0 + (double)eps);
     if (t.n > 0) {
@@ -180,7 +210,7 @@ __global__ void query_kernel(Tree t, const float* __restrict__ q, int k, int mod
             float cur = root_box;
             for (;;) {
                 if (n == 1) {
-                    leaf_visit(t, q, s, mk);
+                    leaf_visit(t, q, dist, s, mk);
                     bool found = false;
                     while (sp > 0) {
                         --sp;
@@ -242,7 +272,7 @@ __global__ void query_kernel(Tree t, const float* __restrict__ q, int k, int mod
                 if ((double)box * max_err >= (double)mk.max_key()) break;
                 for (;;) {
                     if (n == 1) {
-                        leaf_visit(t, q, s, mk);
+                        leaf_visit(t, q, dist, s, mk);
                         break;
                     }
                     const int half = n >> 1, cdim = t.cd[h];
@@ -271,6 +301,124 @@ __global__ void query_kernel(Tree t, const float* __restrict__ q, int k, int mod
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// TFrame.KNNFit for the queries whose tie set exceeds the 64-NN bucket
+// (encoder.lpr:945-958): ANN's priority search (annkPriSearch @0x180011da0,
+// k = 64, eps = 0) over the frame's kd-tree of the 4R candidates, exactly as
+// the DLL runs it -- best-bin-first order, the stable ANNmin_k insert -- so
+// which of the equal-distance candidates fill the bucket, and then the
+// smallest index among the bucket's near-ties, follow the reference.  One
+// thread per query; the bucket lives in LDS, the box queue in HBM.
+// ---------------------------------------------------------------------------
+using OvJob = gsc::KnnOvJob;
+
+constexpr int kOvBlock = 64;
+constexpr int kBucket = 64;  // CBucketSize (encoder.lpr:917)
+
+__global__ __launch_bounds__(kOvBlock) void knnfit_ann_kernel(const Tree* __restrict__ trees,
+                                                               const OvJob* __restrict__ jobs, int njobs,
+                                                               const float* __restrict__ qall, int* __restrict__ out,
+                                                               float* __restrict__ pq_key, int4* __restrict__ pq_node,
+                                                               int pq_cap) {
+    __shared__ float s_key[kOvBlock][kBucket + 1];
+    __shared__ int s_info[kOvBlock][kBucket + 1];
+    const int j = blockIdx.x * kOvBlock + threadIdx.x;
+    if (j >= njobs) return;
+    const OvJob job = jobs[j];
+    const Tree t = trees[job.tree];
+    const float* q = qall + job.q_off;
+    MinK mk{s_key[threadIdx.x], s_info[threadIdx.x], kBucket, 0};
+    float* pk = pq_key + (int64_t)j * pq_cap;
+    int4* pn_ = pq_node + (int64_t)j * pq_cap;
+    int pn = 0;
+    auto pq_insert = [&](float kv, int h, int s, int n) {  // ANNpr_queue::insert (sift up, stop at <=)
+        int r = ++pn;
+        while (r > 1) {
+            const int p = r / 2;
+            if (pk[p] <= kv) break;
+            pk[r] = pk[p];
+            pn_[r] = pn_[p];
+            r = p;
+        }
+        pk[r] = kv;
+        pn_[r] = make_int4(h, s, n, 0);
+    };
+    if (t.n > 0) {
+        pq_insert(box_dist(q, t.bnd, t.bnd + t.dd, t.dd), 0, 0, t.n);
+        while (pn > 0) {
+            const float box = pk[1];
+            const int4 nd = pn_[1];
+            {  // extract_min: last element sifted down (child r+1 iff key[r] > key[r+1]; stop at kn <= key[r])
+                const float kn = pk[pn];
+                const int4 ln = pn_[pn];
+                --pn;
+                int p = 1, r = 2;
+                while (r <= pn) {
+                    if (r < pn && pk[r] > pk[r + 1]) ++r;
+                    if (kn <= pk[r]) break;
+                    pk[p] = pk[r];
+                    pn_[p] = pn_[r];
+                    p = r;
+                    r = p << 1;
+                }
+                pk[p] = kn;
+                pn_[p] = ln;
+            }
+            if ((double)box >= (double)mk.max_key()) break;  // box * (1 + eps)^2, eps = 0
+            int h = nd.x, s = nd.y, n = nd.z;
+            for (;;) {  // ANNkd_split::ann_pri_search: push the far child, descend the near one
+                if (n == 1) {
+                    const float min_dist = mk.max_key();
+                    const int pi = t.pidx[s];
+                    const float* pp = t.pts + (int64_t)pi * t.dd;
+                    float dist = 0.0f;
+                    int d;
+                    for (d = 0; d < t.dd; ++d) {
+                        const float tt = fs(q[d], pp[d]);
+                        if ((dist = fa(dist, fm(tt, tt))) > min_dist) break;
+                    }
+                    if (d >= t.dd) mk.insert(dist, pi);
+                    break;
+                }
+                const int half = n >> 1, cdim = t.cd[h];
+                const float cut = fs(q[cdim], t.cv[h]);
+                float bd;
+                int nh, ns, nn, fh, fs_, fn;
+                if (cut < 0.0f) {
+                    bd = fs(t.lo[h], q[cdim]);
+                    nh = 2 * h + 1; ns = s; nn = half;
+                    fh = 2 * h + 2; fs_ = s + half; fn = n - half;
+                } else {
+                    bd = fs(q[cdim], t.hi[h]);
+                    nh = 2 * h + 2; ns = s + half; nn = n - half;
+                    fh = 2 * h + 1; fs_ = s; fn = half;
+                }
+                if (bd < 0.0f) bd = 0.0f;
+                if (pn + 1 >= pq_cap) {  // cannot happen: at most one push per split node
+                    out[job.out] = -3;
+                    return;
+                }
+                pq_insert(fa(box, fs(fm(cut, cut), fm(bd, bd))), fh, fs_, fn);
+                h = nh; s = ns; n = nn;
+            }
+        }
+    }
+    // tie rule (encoder.lpr:954-958): the smallest index among the bucket's
+    // entries whose sqrt(err / CS) is SameValue with the first one's
+    const float csf = (float)t.dd;
+    int b = mk.n > 0 ? mk.info[0] : -1;
+    const float s0 = mk.n > 0 ? __fsqrt_rn(mk.key[0] / csf) : 0.0f;
+    for (int i = 0; i < mk.n; ++i) {
+        const int id = mk.info[i];
+        if (id >= 0 && id <= b - 1) {
+            const float sj = __fsqrt_rn(mk.key[i] / csf);
+            const float dl = s0 > sj ? fs(s0, sj) : fs(sj, s0);
+            if (dl <= job.eps) b = id;
+        }
+    }
+    out[job.out] = b;
+}
 }  // namespace ann
 }  // namespace gsc
 
@@ -283,10 +431,27 @@ extern "C" hipError_t gsc_launch_ann_build(const float* pts, int n, int dd, int*
 
 extern "C" hipError_t gsc_launch_ann_query(const float* pts, int n, int dd, int* pidx, int* cd, float* cv, float* lo,
                                            float* hi, float* bnd, const float* q, int k, int mode, float eps, int* idxs,
-                                           float* errs, float* mk_key, int* mk_info, float* pq_key, int* pq_h,
-                                           int* pq_s, int* pq_n, hipStream_t st) {
+                                           float* errs, float* dist, float* mk_key, int* mk_info, float* pq_key,
+                                           int* pq_h, int* pq_s, int* pq_n, hipStream_t st) {
     gsc::ann::Tree t{pts, n, dd, pidx, cd, cv, lo, hi, bnd};
-    hipLaunchKernelGGL(gsc::ann::query_kernel, dim3(1), dim3(64), 0, st, t, q, k, mode, eps, idxs, errs, mk_key,
+    hipLaunchKernelGGL(gsc::ann::query_kernel, dim3(1), dim3(1024), 0, st, t, q, k, mode, eps, idxs, errs, dist, mk_key,
                        mk_info, pq_key, pq_h, pq_s, pq_n);
+    return hipGetLastError();
+}
+
+// trees: device array of ntrees descriptors (their arrays already allocated)
+extern "C" hipError_t gsc_launch_ann_build_many(const void* trees, int ntrees, hipStream_t st) {
+    hipLaunchKernelGGL(gsc::ann::build_many_kernel, dim3(ntrees), dim3(64), 0, st,
+                       static_cast<const gsc::ann::Tree*>(trees));
+    return hipGetLastError();
+}
+
+
+extern "C" hipError_t gsc_launch_knnfit_ann(const void* trees, const void* jobs, int njobs, const float* q, int* out,
+                                            float* pq_key, void* pq_node, int pq_cap, hipStream_t st) {
+    const int blocks = (njobs + gsc::ann::kOvBlock - 1) / gsc::ann::kOvBlock;
+    hipLaunchKernelGGL(gsc::ann::knnfit_ann_kernel, dim3(blocks), dim3(gsc::ann::kOvBlock), 0, st,
+                       static_cast<const gsc::ann::Tree*>(trees), static_cast<const gsc::ann::OvJob*>(jobs), njobs, q,
+                       out, pq_key, static_cast<int4*>(pq_node), pq_cap);
     return hipGetLastError();
 }

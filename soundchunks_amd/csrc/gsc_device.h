@@ -56,4 +56,26 @@ struct FitFrame {
     int32_t overflow;     // out: queries whose tie set exceeds ANN's 64-NN bucket
 };
 
+// ANN kd-tree (ANN_KD_STD, bs = 1) over n points, heap-indexed split nodes
+// (gsc_ann.hip): the drop-in ABI's trees and the KNNFit candidate trees.
+struct AnnTree {
+    const float* pts;  // n * dd, row major (the live point values)
+    int n, dd;
+    int* pidx;         // n
+    int* cd;           // heap-indexed split data, 2 * pow2ceil(n) entries
+    float* cv;
+    float* lo;
+    float* hi;
+    float* bnd;        // 2 * dd: bounding rect lo | hi
+};
+
+// One KNNFit query whose tie set exceeds ANN's 64-NN bucket: replayed through
+// ANN's priority search over its frame's candidate tree (gsc_ann.hip).
+struct KnnOvJob {
+    int tree;   // index into the tree array
+    int q_off;  // query: dd floats at q + q_off
+    int out;    // result slot
+    float eps;  // SameValue epsilon of the frame (encoder.lpr:940-943)
+};
+
 }  // namespace gsc

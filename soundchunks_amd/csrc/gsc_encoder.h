@@ -78,6 +78,11 @@ class Encoder {
     // Load + PrepareFrames; returns 0 or a negative error code
     int prepare(const uint8_t* wav, size_t len, std::string* err);
     int frame_count() const { return int(fr_start_.size()); }
+    // chunkRefs count of frame i: chunks x channels (encoder.lpr:467-485)
+    int frame_chunks(int i) const {
+        const int sc = fr_end_[size_t(i)] - fr_start_[size_t(i)] + 1;
+        return ((sc - 1) / opt_.chunk_size + 1) * channels_;
+    }
     // Encode frames [b, e) and return their concatenated stream bytes
     int encode_range(int b, int e, std::vector<uint8_t>* out, std::string* err, gsc_timing* tim);
     // Device DSP of frame f alone (parity tests): attenuation divider and the

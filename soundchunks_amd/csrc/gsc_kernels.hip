@@ -547,6 +547,10 @@ extern "C" hipError_t gsc_launch_scan_pass(int D, ReduceFrame* frames, int nfram
         (void)hipFuncSetAttribute((const void*)scan_pass_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
         hipLaunchKernelGGL(scan_pass_kernel<16>, grid, block, shm, st, frames, nframes, X, C, is, fs, rate_tab, tol, max_passes, only_flagged);
         break;
+    case 32:
+        (void)hipFuncSetAttribute((const void*)scan_pass_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+        hipLaunchKernelGGL(scan_pass_kernel<32>, grid, block, shm, st, frames, nframes, X, C, is, fs, rate_tab, tol, max_passes, only_flagged);
+        break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <new>
 #include <string>
 #include <strings.h>
 #include <thread>
@@ -37,6 +38,9 @@ extern "C" hipError_t gsc_launch_features(int cs, const gsc::DspFrame* frames, i
                                           double scale, float* X, uint8_t* nr, hipStream_t st);
 extern "C" hipError_t gsc_launch_knnfit(int CS, gsc::FitFrame* frames, int nframes, int max_n, int max_r,
                                         const float* cand, const float* q, int* out, hipStream_t st);
+extern "C" hipError_t gsc_launch_ann_build_many(const void* trees, int ntrees, hipStream_t st);
+extern "C" hipError_t gsc_launch_knnfit_ann(const void* trees, const void* jobs, int njobs, const float* q, int* out,
+                                            float* pq_key, void* pq_node, int pq_cap, hipStream_t st);
 
 namespace gsc {
 
@@ -208,7 +212,7 @@ int run_reduce_batch_dev(int D, int K, int precision, const std::vector<int>& Ns
     // launches: one yakmo launch + kMaxScanIters scan launches per batch
     const int nf = int(Ns.size());
     if (nf == 0) return 0;
-    if (D != 8 && D != 16) return fail("KNNScanReduce kernel supports D = 8 or 16 (ChunkSize 4 or 8)");
+    if (D != 8 && D != 16 && D != 32) return fail("KNNScanReduce kernels support D = 8, 16 or 32 (ChunkSize 4, 8, 16)");
     for (int n : Ns)
         if (n > 262144) return fail("frame has more than 262144 chunks (yakmo seeding bitmap)");
     std::vector<ReduceFrame> fr(static_cast<size_t>(nf));
@@ -292,6 +296,110 @@ int run_reduce_batch(int D, int K, int precision, const std::vector<int>& Ns, co
                                 scan_ms);
 }
 
+// KNNFit queries whose tie set exceeds ANN's 64-NN bucket (the brute-force
+// kernel marks them -1): for each affected frame, the 4R candidate rows in
+// the reference order f = 4c + 2neg + rev (encoder.lpr:928-938), ANN's kd-tree
+// over them (the DLL's sequential build), and ANN's priority search + the tie
+// rule for every such query (gsc_ann.hip knnfit_ann_kernel).
+int run_knnfit_overflow(int CS, const std::vector<FitFrame>& fr, const std::vector<int>& ov_frames,
+                        const std::vector<float>& eps, const std::vector<float>& cand, const std::vector<float>& q,
+                        std::vector<int>* best) {
+    const int nt = int(ov_frames.size());
+    std::vector<float> pts;
+    std::vector<int64_t> pt_off(static_cast<size_t>(nt)), nd_off(static_cast<size_t>(nt));
+    std::vector<int> caps(static_cast<size_t>(nt));
+    int64_t nodes = 0;
+    int max_n = 0;
+    for (int t = 0; t < nt; ++t) {
+        const FitFrame& f = fr[size_t(ov_frames[t])];
+        const int n = 4 * f.R;
+        pt_off[t] = int64_t(pts.size());
+        pts.resize(pts.size() + size_t(n) * CS);
+        float* o = pts.data() + pt_off[t];
+        const float* c = cand.data() + f.cand_off;
+        for (int r = 0; r < f.R; ++r) {
+            const float* v = c + size_t(r) * CS;
+            for (int j = 0; j < CS; ++j) {
+                const float fw = v[j], rv = v[CS - 1 - j];
+                // makeFloatSample of the negated int16: exact negation, but 0 stays +0
+                o[(size_t(4 * r) + 0) * CS + j] = fw;
+                o[(size_t(4 * r) + 1) * CS + j] = rv;
+                o[(size_t(4 * r) + 2) * CS + j] = fw == 0.0f ? 0.0f : -fw;
+                o[(size_t(4 * r) + 3) * CS + j] = rv == 0.0f ? 0.0f : -rv;
+            }
+        }
+        int p2 = 1;
+        while (p2 < n) p2 <<= 1;
+        caps[t] = 2 * p2;
+        nd_off[t] = nodes;
+        nodes += caps[t];
+        max_n = std::max(max_n, n);
+    }
+    // jobs: every query the brute-force kernel flagged
+    std::vector<KnnOvJob> jobs;
+    std::vector<int64_t> job_q;
+    for (int t = 0; t < nt; ++t) {
+        const FitFrame& f = fr[size_t(ov_frames[t])];
+        for (int i = 0; i < f.N; ++i)
+            if ((*best)[size_t(f.out_off + i)] == -1) {
+                jobs.push_back(KnnOvJob{t, int(f.q_off + int64_t(i) * CS), int(f.out_off + i), eps[size_t(ov_frames[t])]});
+            }
+    }
+    if (jobs.empty()) return 0;
+    if (q.size() > size_t(INT32_MAX)) return fail("KNNFit overflow: query slab exceeds 2^31 floats");
+    DevBuf<float> dPts, dCv, dLo, dHi, dBnd, dQ, dPqk;
+    DevBuf<int> dPidx, dCd, dOut;
+    DevBuf<AnnTree> dTrees;
+    DevBuf<KnnOvJob> dJobs;
+    DevBuf<int4> dPqn;
+    HIP_TRY(dPts.alloc(pts.size()));
+    HIP_TRY(dPidx.alloc(size_t(pts.size() / size_t(CS))));
+    HIP_TRY(dCd.alloc(size_t(nodes)));
+    HIP_TRY(dCv.alloc(size_t(nodes)));
+    HIP_TRY(dLo.alloc(size_t(nodes)));
+    HIP_TRY(dHi.alloc(size_t(nodes)));
+    HIP_TRY(dBnd.alloc(size_t(2 * CS * nt)));
+    HIP_TRY(dTrees.alloc(size_t(nt)));
+    HIP_TRY(dQ.alloc(q.size()));
+    HIP_TRY(dOut.alloc(best->size()));
+    HIP_TRY(hipMemcpy(dPts.p, pts.data(), sizeof(float) * pts.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemset(dCd.p, 0xff, sizeof(int) * size_t(nodes)));
+    HIP_TRY(hipMemcpy(dQ.p, q.data(), sizeof(float) * q.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dOut.p, best->data(), sizeof(int) * best->size(), hipMemcpyHostToDevice));
+    std::vector<AnnTree> trees(static_cast<size_t>(nt));
+    for (int t = 0; t < nt; ++t) {
+        AnnTree& a = trees[size_t(t)];
+        a.pts = dPts.p + pt_off[t];
+        a.n = 4 * fr[size_t(ov_frames[t])].R;
+        a.dd = CS;
+        a.pidx = dPidx.p + pt_off[t] / CS;
+        a.cd = dCd.p + nd_off[t];
+        a.cv = dCv.p + nd_off[t];
+        a.lo = dLo.p + nd_off[t];
+        a.hi = dHi.p + nd_off[t];
+        a.bnd = dBnd.p + size_t(2 * CS) * size_t(t);
+    }
+    HIP_TRY(hipMemcpy(dTrees.p, trees.data(), sizeof(AnnTree) * size_t(nt), hipMemcpyHostToDevice));
+    HIP_TRY(gsc_launch_ann_build_many(dTrees.p, nt, nullptr));
+    // the box queues (<= one push per split node each): bounded launches
+    const int pq_cap = max_n + 2;
+    const size_t per_job = size_t(pq_cap) * (sizeof(float) + sizeof(int4));
+    const int chunk = int(std::max<size_t>(64, std::min<size_t>(jobs.size(), (size_t(2) << 30) / per_job)));
+    HIP_TRY(dPqk.alloc(size_t(chunk) * pq_cap));
+    HIP_TRY(dPqn.alloc(size_t(chunk) * pq_cap));
+    HIP_TRY(dJobs.alloc(jobs.size()));
+    HIP_TRY(hipMemcpy(dJobs.p, jobs.data(), sizeof(KnnOvJob) * jobs.size(), hipMemcpyHostToDevice));
+    for (size_t j0 = 0; j0 < jobs.size(); j0 += size_t(chunk)) {
+        const int nj = int(std::min<size_t>(size_t(chunk), jobs.size() - j0));
+        HIP_TRY(gsc_launch_knnfit_ann(dTrees.p, dJobs.p + j0, nj, dQ.p, dOut.p, dPqk.p, dPqn.p, pq_cap, nullptr));
+    }
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(best->data(), dOut.p, sizeof(int) * best->size(), hipMemcpyDeviceToHost));
+    for (const KnnOvJob& j : jobs)
+        if ((*best)[size_t(j.out)] < 0) return fail("KNNFit: ANN priority search emulation failed");
+    return 0;
+}
+
 int run_knnfit_batch(int CS, const std::vector<int>& Rs, const std::vector<int>& Ns, const std::vector<float>& eps,
                      const std::vector<float>& cand, const std::vector<float>& q, std::vector<int>* best,
                      double* knn_ms) {
@@ -338,10 +446,14 @@ int run_knnfit_batch(int CS, const std::vector<int>& Rs, const std::vector<int>&
     best->resize(size_t(qo / CS));
     HIP_TRY(hipMemcpy(best->data(), dOut.p, sizeof(int) * best->size(), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(fr.data(), dFr.p, sizeof(FitFrame) * size_t(nf), hipMemcpyDeviceToHost));
+    std::vector<int> ov_frames;
     for (int i = 0; i < nf; ++i)
-        if (fr[i].overflow > 0)
-            return fail("KNNFit: " + std::to_string(fr[i].overflow) +
-                        " queries tie with more than 64 candidates (ANN bucket order emulation pending)");
+        if (fr[i].overflow > 0) ov_frames.push_back(i);
+    if (!ov_frames.empty()) {
+        const double t0 = now_ms();
+        if (run_knnfit_overflow(CS, fr, ov_frames, eps, cand, q, best) != 0) return -1;
+        if (knn_ms) *knn_ms += now_ms() - t0;
+    }
     return 0;
 }
 
@@ -655,6 +767,26 @@ int gsc_count_frames(const uint8_t* wav, size_t wav_len, const gsc_options* o, i
     return 0;
 }
 
+// encode frames [frame_begin, frame_end) of a prepared encoder into a
+// library-allocated buffer; timing lands in t_tim (host_prepare_ms excluded)
+static int encode_prepared(Encoder& enc, int frame_begin, int frame_end, uint8_t** out, size_t* out_len) {
+    const double t0 = now_ms();
+    const int fc = enc.frame_count();
+    frame_begin = std::max(0, frame_begin);
+    frame_end = std::min(fc, frame_end < 0 ? fc : frame_end);
+    std::vector<uint8_t> bytes;
+    std::string err;
+    if (frame_end > frame_begin) {
+        if (enc.encode_range(frame_begin, frame_end, &bytes, &err, &t_tim) != 0) return fail(err);
+    }
+    *out = static_cast<uint8_t*>(std::malloc(std::max<size_t>(bytes.size(), 1)));
+    if (!*out) return fail("out of host memory");
+    if (!bytes.empty()) std::memcpy(*out, bytes.data(), bytes.size());
+    *out_len = bytes.size();
+    t_tim.total_ms = now_ms() - t0;
+    return 0;
+}
+
 int gsc_encode_wav_frames(const uint8_t* wav, size_t wav_len, const gsc_options* o, int frame_begin, int frame_end,
                           uint8_t** out, size_t* out_len, int* frame_count) {
     const double t0 = now_ms();
@@ -663,21 +795,65 @@ int gsc_encode_wav_frames(const uint8_t* wav, size_t wav_len, const gsc_options*
     std::string err;
     if (enc.prepare(wav, wav_len, &err) != 0) return fail(err);
     const double t1 = now_ms();
-    const int fc = enc.frame_count();
-    if (frame_count) *frame_count = fc;
-    frame_begin = std::max(0, frame_begin);
-    frame_end = std::min(fc, frame_end < 0 ? fc : frame_end);
-    std::vector<uint8_t> bytes;
-    if (frame_end > frame_begin) {
-        if (enc.encode_range(frame_begin, frame_end, &bytes, &err, &t_tim) != 0) return fail(err);
-    }
-    *out = static_cast<uint8_t*>(std::malloc(std::max<size_t>(bytes.size(), 1)));
-    if (!bytes.empty()) std::memcpy(*out, bytes.data(), bytes.size());
-    *out_len = bytes.size();
+    if (frame_count) *frame_count = enc.frame_count();
+    if (encode_prepared(enc, frame_begin, frame_end, out, out_len) != 0) return -1;
     t_tim.host_prepare_ms = t1 - t0;
     t_tim.total_ms = now_ms() - t0;
     return 0;
 }
+
+}  // extern "C"
+
+// a WAV after Load + PrepareFrames: the frame boundaries of the whole file,
+// computed once per job and shared by every frame-range encode (sharding)
+struct gsc_prepared {
+    Encoder enc;
+    double prepare_ms = 0;
+    explicit gsc_prepared(const gsc_options& o) : enc(o) {}
+};
+
+extern "C" {
+
+gsc_prepared* gsc_prepare(const uint8_t* wav, size_t wav_len, const gsc_options* o) {
+    if (!wav || !o) {
+        fail("gsc_prepare: null argument");
+        return nullptr;
+    }
+    const double t0 = now_ms();
+    gsc_prepared* p = new (std::nothrow) gsc_prepared(*o);
+    if (!p) {
+        fail("gsc_prepare: out of host memory");
+        return nullptr;
+    }
+    std::string err;
+    if (p->enc.prepare(wav, wav_len, &err) != 0) {
+        delete p;
+        fail(err);
+        return nullptr;
+    }
+    p->prepare_ms = now_ms() - t0;
+    return p;
+}
+
+int gsc_prepared_frame_count(const gsc_prepared* p) { return p ? p->enc.frame_count() : -1; }
+
+int gsc_prepared_frame_chunks(const gsc_prepared* p, int* chunks) {
+    if (!p || !chunks) return fail("gsc_prepared_frame_chunks: null argument");
+    for (int i = 0; i < p->enc.frame_count(); ++i) chunks[i] = p->enc.frame_chunks(i);
+    return 0;
+}
+
+int gsc_encode_prepared(gsc_prepared* p, int frame_begin, int frame_end, uint8_t** out, size_t* out_len) {
+    if (!p || !out || !out_len) return fail("gsc_encode_prepared: null argument");
+    t_tim = gsc_timing{};
+    if (encode_prepared(p->enc, frame_begin, frame_end, out, out_len) != 0) return -1;
+    t_tim.host_prepare_ms = 0;  // paid once, in gsc_prepare
+    return 0;
+}
+
+double gsc_prepared_prepare_ms(const gsc_prepared* p) { return p ? p->prepare_ms : 0.0; }
+
+void gsc_prepared_free(gsc_prepared* p) { delete p; }
 
 int gsc_frame_dsp(const uint8_t* wav, size_t wav_len, const gsc_options* o, int frame, int* atten_div, float** feat,
                   int* n_chunks) {
@@ -736,7 +912,7 @@ int gsc_scan_reduce(int n, int d, const float* x, int k, float* centroids, int* 
     if (ensure_device() != 0) return -1;
     // same kernels as the encoder, but starting from caller-provided centroids:
     // seed via yakmo is skipped by uploading the centroids after the yakmo launch
-    if (d != 8 && d != 16) return fail("KNNScanReduce kernel supports D = 8 or 16");
+    if (d != 8 && d != 16 && d != 32) return fail("KNNScanReduce kernels support D = 8, 16 or 32");
     std::vector<ReduceFrame> fr(1);
     fr[0] = ReduceFrame{};
     fr[0].N = n;

@@ -67,11 +67,58 @@ class Encoder:
         finally:
             lib.gsc_free(out)
 
+    def prepare(self, wav: bytes) -> "Prepared":
+        """Load + PrepareFrames once (the frame boundaries of the whole file)."""
+        return Prepared(self, wav)
+
     @staticmethod
     def last_timing() -> dict:
         t = _lib.GscTiming()
         _lib.load().gsc_last_timing(ctypes.byref(t))
         return {k: getattr(t, k) for k, _ in t._fields_}
+
+
+class Prepared:
+    """A WAV after TEncoder.Load + PrepareFrames (encoder.lpr:1111-1152,
+    1294-1429): frame boundaries computed once per job, then any frame range
+    encodes without rescanning the file (multi-GPU sharding)."""
+
+    def __init__(self, encoder: Encoder, wav: bytes):
+        lib = _lib.load()
+        arr, ptr = _u8(wav)
+        h = lib.gsc_prepare(ptr, len(arr), ctypes.byref(encoder.options))
+        if not h:
+            raise _lib.GscError(lib.gsc_last_error().decode(errors="replace"))
+        self._h = h
+        self.frame_count = lib.gsc_prepared_frame_count(h)
+        self.prepare_ms = lib.gsc_prepared_prepare_ms(h)
+
+    def frame_chunks(self) -> np.ndarray:
+        """chunkRefs count (chunks x channels) per frame: the sharding weights."""
+        out = np.zeros(max(1, self.frame_count), dtype=np.int32)
+        _lib.check(_lib.load().gsc_prepared_frame_chunks(self._h, _ip(out)))
+        return out[: self.frame_count]
+
+    def encode(self, frame_begin: int = 0, frame_end: int = -1) -> bytes:
+        lib = _lib.load()
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_size_t(0)
+        _lib.check(lib.gsc_encode_prepared(self._h, frame_begin, frame_end, ctypes.byref(out), ctypes.byref(n)))
+        try:
+            return ctypes.string_at(out, n.value)
+        finally:
+            lib.gsc_free(out)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            _lib.load().gsc_prepared_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def set_device(device: int) -> None:

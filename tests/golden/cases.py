@@ -33,6 +33,21 @@ def _silence_tone(seconds=2.0, rate=44100):
     return wav_header(1, rate, n) + pcm.tobytes()
 
 
+def _quiet_tone(seconds=3.0, frac=0.6, rate=44100, seed=5):
+    """Mono: +-1 LSB noise for the first `frac`, then a tone.  Thousands of
+    reduced chunks quantise to all zeros, so KNNFit queries in the quiet part
+    tie with far more than 64 candidates: ANN's bucket order decides them
+    (encoder.lpr:945-958)."""
+    from soundchunks_amd.synth import wav_header
+
+    rng = np.random.default_rng(seed)
+    n = int(seconds * rate)
+    t = np.arange(n) / rate
+    x = np.round(0.3 * np.sin(2 * np.pi * 330 * t) * 32767).astype(np.int64)
+    x = np.where(t < seconds * frac, rng.integers(-1, 2, size=n), x)
+    return wav_header(1, rate, n) + x.astype("<i2").tobytes()
+
+
 def _tiny():
     """0.02 s: fewer chunks than ChunksPerFrame -> passthrough mode (encoder.lpr:891-912)."""
     return _synth(0.02)
@@ -47,6 +62,16 @@ CASES = {
     "syn3s_cs8_cpf1000_cbd12": (lambda: _synth(3.0), ["-cs8", "-cpf1000", "-cbd12"]),
     "silence_tone_cs8_cpf256": (lambda: _silence_tone(), ["-cs8", "-cpf256"]),
     "tiny_passthrough_cs8": (lambda: _tiny(), ["-cs8", "-cpf256"]),
+    # KNNFit tie sets beyond the 64-NN bucket (ANN priority-search order)
+    "quiet_tone_cs8_cpf1024": (lambda: _quiet_tone(), ["-cs8", "-cpf1024"]),
+    "quiet_tone_cs4_cpf1024": (lambda: _quiet_tone(frac=0.9), ["-cs4", "-cpf1024"]),
+    # C2 at the benchmark's frame shape: two full 4-s frames (N = 44100 each) in one launch
+    "syn8s_c2_cs8_cpf4096": (lambda: _synth(8.0), ["-cs8", "-cpf4096", "-cbd8"]),
+    # C3: ChunkSize 16 (D = 32 features), 12-bit, two N = 22050 frames
+    "syn8s_c3_cs16_cpf4096_cbd12": (lambda: _synth(8.0), ["-cs16", "-cpf4096", "-cbd12"]),
+    # C5: 48 kHz stereo at ChunkCount 4096, the encoder default ChunkSize 4 and 8
+    "syn8s_48k_cs4_cpf4096": (lambda: _synth(8.0, 48000), ["-cs4", "-cpf4096"]),
+    "syn8s_48k_cs8_cpf4096": (lambda: _synth(8.0, 48000), ["-cs8", "-cpf4096"]),
 }
 
 

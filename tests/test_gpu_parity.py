@@ -58,6 +58,27 @@ def test_knnfit_bit_exact(oracle, name):
     np.testing.assert_array_equal(best, tr["knn_best"])
 
 
+@pytest.mark.parametrize("name", ["quiet_tone_cs8_cpf1024", "quiet_tone_cs4_cpf1024"])
+def test_knnfit_bucket_overflow_follows_ann_order(oracle, name):
+    """Queries in near-silence tie with thousands of all-zero candidates: the
+    64-NN bucket holds the first 64 ANN's priority search meets, and the tie
+    rule picks the smallest index among those (encoder.lpr:945-958) -- the
+    GPU path replays that search for exactly these queries."""
+    import soundchunks_amd as sc
+
+    tr = _trace(oracle, name)
+    cand, q, eps, cs = tr["knn_cand"], tr["knn_query"], tr["knn_eps"], tr["CS"]
+    # the case must actually overflow the bucket (> 64 candidates within eps)
+    zero = int((np.abs(cand).sum(axis=1) == 0).sum())
+    assert zero > 64
+    best = sc.knnfit_assign(cand[0::4], q, eps)
+    np.testing.assert_array_equal(best, tr["knn_best"])
+    # a brute-force "smallest index among all ties" differs on some of them
+    quiet = np.abs(q).sum(axis=1) == 0
+    assert quiet.any()
+    assert (tr["knn_best"][quiet] > np.flatnonzero(np.abs(cand).sum(axis=1) == 0)[0]).any()
+
+
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_gsc_matches_golden(name):
     import soundchunks_amd as sc

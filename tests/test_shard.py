@@ -72,3 +72,47 @@ def test_two_rank_gather_equals_single_encode():
     assert fc >= 3
     want = oracle_ffi.encode(synth_wav(seconds, 44100, 1), argv, threads=4)
     assert got == want
+
+
+def _hip_worker(rank, ws, port, name, q):
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    import soundchunks_amd as sc
+    from golden.cases import CASES
+    from soundchunks_amd.shard import frame_range_weighted, gather_streams
+
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        make, argv = CASES[name]
+        prep = sc.Encoder(argv).prepare(make())  # PrepareFrames once per job
+        b, e = frame_range_weighted(prep.frame_chunks().tolist(), rank, ws)
+        out = gather_streams(prep.encode(b, e))
+        if rank == 0:
+            q.put((prep.frame_count, (b, e), out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_two_rank_hip_encoder_matches_golden():
+    """The HIP encoder in 2 gloo ranks (both on device 0): each rank encodes its
+    chunk-count-balanced frame range; rank 0's gathered bytes equal the golden."""
+    from golden.cases import golden_path
+
+    name = "c1_test_cs8_cpf256"
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30500 + (os.getpid() % 1000)
+    procs = [ctx.Process(target=_hip_worker, args=(r, 2, port, name, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    fc, rng0, got = q.get(timeout=280)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert fc >= 3 and 0 < rng0[1] < fc
+    assert got == golden_path(name).read_bytes()
