@@ -103,7 +103,8 @@ struct ann_kdtree_t {
     int* h_out = nullptr;      // pinned: idxs | errs of the last search
 
     void release() {
-        for (float** p : {&d_pts, &d_cv, &d_lo, &d_hi, &d_bnd, &d_q, &d_dist, &d_err, &d_mk, &d_pqk}) dfree(*p);
+        d_q = nullptr;  // aliases the tail of d_pts
+        for (float** p : {&d_pts, &d_cv, &d_lo, &d_hi, &d_bnd, &d_dist, &d_err, &d_mk, &d_pqk}) dfree(*p);
         for (int** p : {&d_pidx, &d_cd, &d_idx, &d_mki, &d_pqh, &d_pqs, &d_pqn}) dfree(*p);
         if (h_stage) (void)hipHostFree(h_stage);
         if (h_out) (void)hipHostFree(h_out);
@@ -183,9 +184,20 @@ static void stage_points(ann_kdtree_t* t, const float* q, const char* fn) {
 }
 
 ann_kdtree_t* ann_kdtree_create(float** pa, int n, int dd, int bs, int split) {
+    static const char* fn = "ann_kdtree_create";
     if (bs != 1 || split != 0 || n < 0 || dd <= 0 || (n > 0 && !pa)) return nullptr;  // only bs = 1, ANN_KD_STD
-    if (!device_ok()) return nullptr;
+    if (!device_ok()) {
+        std::fprintf(stderr, "soundchunks_amd: %s: no gfx950 device (no CPU fallback)\n", fn);
+        return nullptr;
+    }
     ann_kdtree_t* t = new ann_kdtree_t();
+    auto give_up = [&](const char* why, hipError_t e) -> ann_kdtree_t* {
+        std::fprintf(stderr, "soundchunks_amd: %s: %s: %s\n", fn, why, hipGetErrorString(e));
+        (void)hipGetLastError();  // do not leave the failure to the next launch check
+        t->release();
+        delete t;
+        return nullptr;
+    };
     t->pa = pa;
     t->n = n;
     t->dd = dd;
@@ -205,28 +217,22 @@ ann_kdtree_t* ann_kdtree_create(float** pa, int n, int dd, int bs, int split) {
     t->d_pqh = dalloc<int>(size_t(n) + 2);
     t->d_pqs = dalloc<int>(size_t(n) + 2);
     t->d_pqn = dalloc<int>(size_t(n) + 2);
-    const bool host_ok = hipHostMalloc(reinterpret_cast<void**>(&t->h_stage), 4 * (size_t(n) + 1) * dd) == hipSuccess;
-    if (!host_ok || !t->d_pts || !t->d_pidx || !t->d_cd || !t->d_cv || !t->d_lo || !t->d_hi || !t->d_bnd ||
-        !t->d_dist || !t->d_pqk || !t->d_pqh || !t->d_pqs || !t->d_pqn) {
-        t->release();
-        delete t;
-        return nullptr;
+    if (!t->d_pts || !t->d_pidx || !t->d_cd || !t->d_cv || !t->d_lo || !t->d_hi || !t->d_bnd || !t->d_dist ||
+        !t->d_pqk || !t->d_pqh || !t->d_pqs || !t->d_pqn)
+        return give_up("device allocation", hipErrorOutOfMemory);
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&t->h_stage), 4 * (size_t(n) + 1) * dd, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        t->h_stage = nullptr;
+        return give_up("pinned staging allocation", e);
     }
     t->d_q = t->d_pts + size_t(n) * dd;
-    if (hipMemset(t->d_cd, 0xff, 4 * size_t(t->cap)) != hipSuccess) {
-        t->release();
-        delete t;
-        return nullptr;
-    }
+    if ((e = hipMemset(t->d_cd, 0xff, 4 * size_t(t->cap))) != hipSuccess) return give_up("hipMemset", e);
     if (n > 0) {
-        stage_points(t, nullptr, "ann_kdtree_create");
-        if (gsc_launch_ann_build(t->d_pts, n, dd, t->d_pidx, t->d_cd, t->d_cv, t->d_lo, t->d_hi, t->d_bnd, nullptr) !=
-                hipSuccess ||
-            hipDeviceSynchronize() != hipSuccess) {
-            t->release();
-            delete t;
-            return nullptr;
-        }
+        stage_points(t, nullptr, fn);
+        if ((e = gsc_launch_ann_build(t->d_pts, n, dd, t->d_pidx, t->d_cd, t->d_cv, t->d_lo, t->d_hi, t->d_bnd,
+                                      nullptr)) != hipSuccess)
+            return give_up("tree build launch", e);
+        if ((e = hipDeviceSynchronize()) != hipSuccess) return give_up("tree build", e);
     }
     return t;
 }
@@ -247,7 +253,10 @@ static void ann_query(ann_kdtree_t* t, int* idxs, float* errs, int cnt, const fl
         float* nm = dalloc<float>(size_t(cnt) + 1);
         int* nmi = dalloc<int>(size_t(cnt) + 1);
         int* ho = nullptr;
-        if (hipHostMalloc(reinterpret_cast<void**>(&ho), 8 * size_t(cnt)) != hipSuccess) ho = nullptr;
+        if (hipHostMalloc(reinterpret_cast<void**>(&ho), 8 * size_t(cnt), hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            ho = nullptr;
+        }
         if (!ni || !ne || !nm || !nmi || !ho) {
             dfree(ni);
             dfree(ne);

@@ -167,7 +167,6 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
         float q[D];
 #pragma unroll
         for (int d = 0; d < D; ++d) q[d] = qp[d];
-        const float qlane = qp[lane & (D - 1)];
         const float rootbox = box0[i];
         // ---- phase A: live distances of this lane's 8 kd leaves ----
         float dv[kScanSlots];
@@ -258,7 +257,10 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
                 }
                 if (n >= 2) {
                     const int cdim = sh.t.cd[h];
-                    const float qc = __shfl(qlane, cdim);
+                    // q[cdim] straight from the query row: a cross-lane read
+                    // here would source lanes >= maxdepth, which are inactive
+                    // in this branch (cut dims reach D - 1 = 31 at ChunkSize 16)
+                    const float qc = qp[cdim];
                     const float cut = fsub(qc, sh.t.cv[h]);
                     const bool nearlo = cut < 0.0f;
                     if (golo != nearlo) {
@@ -268,8 +270,6 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
                         inc = fsub(fmul(cut, cut), fmul(bd, bd));
                     }
                 }
-            } else {
-                (void)__shfl(qlane, 0);
             }
             const uint64_t farmask = __ballot(far);
             // box' = ((root + inc_a) + inc_b) + ... over far steps, in depth order

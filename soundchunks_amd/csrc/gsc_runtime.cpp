@@ -30,7 +30,8 @@ extern "C" hipError_t gsc_launch_scan_pass(int D, gsc::ReduceFrame* frames, int 
                                            int only_flagged, hipStream_t st);
 extern "C" hipError_t gsc_launch_scan_batch(int D, int logk, gsc::ReduceFrame* frames, int nframes, const float* X,
                                             float* C, int* is, const float* rate_tab, double tol, int max_passes,
-                                            hipStream_t st);
+                                            uint64_t* xbuf, hipStream_t st);
+extern "C" size_t gsc_scan_xbuf_granules_per_frame(void);
 extern "C" hipError_t gsc_launch_atten(int cs, gsc::DspFrame* frames, int nframes, const double* samp, int64_t span,
                                        int ch, int obd, hipStream_t st);
 extern "C" hipError_t gsc_launch_features(int cs, const gsc::DspFrame* frames, int nframes, int max_n,
@@ -117,6 +118,7 @@ int ensure_device() {
         }
     }
     if (state < 0) return fail(why);
+    (void)hipGetLastError();  // a failure of an earlier unrelated call must not fail this one's launch checks
     return 0;
 }
 
@@ -149,12 +151,16 @@ double scan_tolerance(int precision) {
     return 1.0 / p;
 }
 
-// K = 2^logk in [256, 4096] and D in {8, 16}: the batched speculative kernel
-// (gsc_scan.hip) covers the pass; anything else runs the generic kernel.
+// K = 2^logk in [256, 4096] and D in {8, 16, 32}: the batched speculative
+// kernel (gsc_scan.hip) covers the pass; anything else runs the generic kernel.
 bool batched_scan_shape(int D, int K) {
     if (std::getenv("GSC_SCAN_GENERIC")) return false;  // diagnostic switch
-    return (D == 8 || D == 16) && K >= 256 && K <= 4096 && (K & (K - 1)) == 0;
+    return (D == 8 || D == 16 || D == 32) && K >= 256 && K <= 4096 && (K & (K - 1)) == 0;
 }
+
+// D = 32 at K = 4096 runs each frame on two CUs, which hand data over through
+// zeroed per-frame granule slots
+bool two_cu_frames(int D, int K) { return D == 32 && K == 4096; }
 
 // launch rounds of launch_scan_passes since the last reset (bench: launches
 // of the dominant kernel)
@@ -167,6 +173,13 @@ hipError_t launch_scan_passes(int D, ReduceFrame* dfr, int nf, int K, const floa
                               const float* rate, int precision) {
     const double tol = scan_tolerance(precision);
     const bool batched = batched_scan_shape(D, K);
+    DevBuf<uint64_t> xbuf;
+    if (batched && two_cu_frames(D, K)) {
+        const size_t n = gsc_scan_xbuf_granules_per_frame() * size_t(nf);
+        hipError_t e = xbuf.alloc(n);
+        if (e == hipSuccess) e = hipMemset(xbuf.p, 0, sizeof(uint64_t) * n);
+        if (e != hipSuccess) return e;
+    }
     int logk = 0;
     while ((1 << logk) < K) ++logk;
     int max_passes = kMaxScanIters;
@@ -177,7 +190,7 @@ hipError_t launch_scan_passes(int D, ReduceFrame* dfr, int nf, int K, const floa
     std::vector<int32_t> done(static_cast<size_t>(nf));
     for (int round = 0; round < max_passes; ++round) {
         if (batched) {
-            const hipError_t e = gsc_launch_scan_batch(D, logk, dfr, nf, X, C, is, rate, tol, max_passes, nullptr);
+            const hipError_t e = gsc_launch_scan_batch(D, logk, dfr, nf, X, C, is, rate, tol, max_passes, xbuf.p, nullptr);
             if (e != hipSuccess) return e;
         }
         const hipError_t e = gsc_launch_scan_pass(D, dfr, nf, K, X, C, is, fs, rate, tol, max_passes, batched ? 1 : 0, nullptr);

@@ -1,5 +1,5 @@
-// KNNScanReduce (encoder.lpr:699-765) as a batched, speculative pipeline on
-// one CU per frame -- the hot kernel of the SoundChunks encode path.
+// KNNScanReduce (encoder.lpr:699-765) as a batched, speculative pipeline --
+// the hot kernel of the SoundChunks encode path.
 //
 // Reference semantics: per pass, ANN builds a kd-tree over the centroids
 // (ann_kdtree_create, encoder.lpr:729) and then, for every point i in order,
@@ -9,16 +9,25 @@
 // update of point i, so the chain is sequential.  Only ONE centroid moves per
 // point, which is what this kernel exploits.
 //
-// Layout: the K = 2^LOGK centroids live in VGPRs, 8 consecutive kd-leaf
-// positions per lane (K = 4096: 8 waves x 64 lanes x 8 x D floats), so leaf
-// position p = (wave*64 + lane)*8 + slot and every kd subtree is an aligned
-// block of waves / lanes / slots.
+// Layout: the K = 2^LOGK centroids live in VGPRs, SL consecutive kd-leaf
+// positions per lane, so every kd subtree is an aligned block of (virtual)
+// waves, lanes and slots: leaf position p = (vwave*64 + lane)*SL + slot.
+//   D <= 16 (ChunkSize 4, 8): one CU per frame, SL = 8 (K = 4096: 8 waves x
+//            64 lanes x 8 leaves x D floats).
+//   D = 32 (ChunkSize 16): 4096 x 32 floats are 512 KB, the whole register
+//            file of a CU, so a frame runs on TWO CUs (NWG = 2), each holding
+//            half of the leaves (the kd root's two subtrees), SL = 4, as one
+//            virtual workgroup of 16 waves.  Both workgroups run the same
+//            pipeline on the same LDS state; what only one of them can compute
+//            (A1 records of its waves, coordinates of its leaves, exact
+//            distances of its leaves) is handed over through HBM as tagged
+//            8-byte granules (xchg below).  K <= 2048 at D = 32 fits one CU
+//            with SL = 4.
 //
-// Pipeline, per iteration (batches of kBatch queries; "current" = the batch
+// Pipeline, per iteration (batches of KB queries; "current" = the batch
 // whose distances are computed now, "pending" = the previous batch, whose
 // speculative answers are committed now):
-//   part 1  A1 (all waves): snapshot distances of the current batch: each lane
-//           computes its 8 leaf distances (bit-exact sequential f32, no FMA);
+//   part 1  A1 (all waves): snapshot distance bounds of the current batch;
 //           a wave min-tree (DPP) gives per wave the minimum, a tie flag, the
 //           argmin position and the minimum of every sibling subtree on the
 //           path to it.  Wave 0 first chains the pending batch's online
@@ -34,8 +43,8 @@
 //           residual in order, update log), choose the next batch.
 //   part 4  owners fold the log into their registers.
 // A query that fails restarts the pipeline at that query on a fresh snapshot;
-// if it fails on a fresh snapshot it is resolved by the exact single-lane DFS
-// (dfs_exact) over live distances.
+// if it fails on a fresh snapshot it is resolved by the exact parallel DFS
+// (dfs_parallel) over live distances.
 //
 // Certificate (why c* is ANN's answer): c* is the unique global minimum; ANN
 // visits c* iff at every far step u on c*'s root path box'(u) < best-so-far;
@@ -49,9 +58,29 @@
 
 namespace gsc {
 
-constexpr int kBatch = 32;         // queries per speculative batch (log window 2*kBatch <= 64)
-constexpr int kVer = 64 + kBatch;  // centroid versions seen by a pending batch
-constexpr int kRow = 20;           // coordinate row stride of lane-indexed LDS rows (80 B: no b128 bank conflicts)
+// Shape of one KNNScanReduce pipeline instance.
+template <int D_, int LOGK_, int SL_, int NWG_>
+struct ScanCfg {
+    static constexpr int D = D_, LOGK = LOGK_, SL = SL_, NWG = NWG_;
+    static constexpr int K = 1 << LOGK;
+    static constexpr int LS = SL == 8 ? 3 : (SL == 4 ? 2 : 1);        // log2 slots per lane
+    static constexpr int LPW = 64 * SL;                                 // leaves per wave
+    static constexpr int KG = K / NWG;                                  // leaves per workgroup
+    static constexpr bool FULL = KG >= LPW;                             // every lane holds SL leaves
+    static constexpr int NWL = FULL ? KG / LPW : 1;                     // waves per workgroup
+    static constexpr int NWV = NWL * NWG;                               // virtual waves
+    static constexpr int NT = 64 * NWL;                                 // threads per workgroup
+    static constexpr int KW = LOGK - 6 - LS >= 0 ? LOGK - 6 - LS : 0;   // kd depths resolved at wave level
+    static constexpr int KB = D > 16 ? 16 : 32;                         // queries per speculative batch
+    static constexpr int KVER = 64 + KB;                                // centroid versions a pending batch sees
+    static constexpr int QD = D < 16 ? 16 : D;                          // query row stride
+    static constexpr int ROW = D + 4;  // lane-indexed coordinate rows: 16-B multiple, odd x 16 B (no b128 conflicts)
+    // A1 bound slack: eps(q) = (|q|^2 + M) * 2^-EPSX (see a1_dist_x2)
+    static constexpr float EPSF = D > 16 ? 0x1p-16f : 0x1p-17f;
+    static_assert(NWV <= 16, "A2 evaluates up to 16 wave records per query (one per lane of a 16-lane group)");
+    static_assert(KB <= 32 && 64 % KB == 0, "batch size");
+    static_assert(NWG == 1 || (FULL && NWL == 8), "two-CU frames: 8 full waves per workgroup");
+};
 
 // float minimum on f32 bit patterns (A1 values may be negative: the batch
 // queries' bounds are |c|^2 - 2 q.c; exact distances are >= +0, where this
@@ -67,19 +96,21 @@ constexpr uint32_t kInfBits = 0x7F800000u;  // +inf: empty leaf / no value
 __device__ __forceinline__ int ordkey(uint32_t b) { return (int)(b ^ ((uint32_t)((int32_t)b >> 31) >> 1)); }
 __device__ __forceinline__ uint32_t keybits(int k) { return (uint32_t)ordkey((uint32_t)k); }
 
-struct WaveRec {      // A1 output per (wave, query): raw values of the argmin lane L;
+template <int SL>
+struct WaveRecT {     // A1 output per (wave, query): raw values of the argmin lane L;
                       // the winner's path minima are derived in A2 (rec_* below)
-    uint32_t minbits; // wave minimum distance (f32 bits; distances are >= 0)
+    uint32_t minbits; // wave minimum distance (f32 bits)
     int lanebits;     // L | 256 if another lane of the wave also holds the minimum
     uint32_t sl[6];   // lane L's sibling lane-group minima, groups of 2^b lanes (b = 0..5), as order keys
-    uint32_t b[8];    // lane L's 8 leaf distances (slots = kd leaves 8L .. 8L+7 of the wave)
+    uint32_t b[SL];   // lane L's SL leaf values (slots = kd leaves SL*L .. SL*L + SL-1 of the wave)
 };
 
 // first slot of lane L at the wave minimum, and whether another slot ties it
-__device__ __forceinline__ int rec_slot(const WaveRec& r, bool* tie2) {
-    int ls = 7, lc = 0;
+template <int SL>
+__device__ __forceinline__ int rec_slot(const WaveRecT<SL>& r, bool* tie2) {
+    int ls = SL - 1, lc = 0;
 #pragma unroll
-    for (int s = 7; s >= 0; --s) {
+    for (int s = SL - 1; s >= 0; --s) {
         const bool e = r.b[s] == r.minbits;
         lc += e ? 1 : 0;
         ls = e ? s : ls;
@@ -89,19 +120,21 @@ __device__ __forceinline__ int rec_slot(const WaveRec& r, bool* tie2) {
 }
 
 // sibling-subtree minimum on the path to slot ls: lane groups (idx 0..5),
-// sibling slot (6), other slot pair of the quad (7), other quad (8)
-__device__ __forceinline__ uint32_t rec_sib(const WaveRec& r, int ls, int idx) {
+// sibling slot (6), other slot pair (7), other quad (8, SL = 8 only)
+template <int SL>
+__device__ __forceinline__ uint32_t rec_sib(const WaveRecT<SL>& r, int ls, int idx) {
     if (idx < 6) return keybits((int)r.sl[idx]);
     if (idx == 6) return r.b[ls ^ 1];
-    if (idx == 7) {
-        const int pb = (ls & 4) | ((ls & 2) ^ 2);
+    if (SL == 4 || idx == 7) {
+        const int pb = (ls & (SL - 4)) | ((ls & 2) ^ 2);
         return fminb(r.b[pb], r.b[pb + 1]);
     }
     const int qb = (ls & 4) ^ 4;
     return fminb(fminb(r.b[qb], r.b[qb + 1]), fminb(r.b[qb + 2], r.b[qb + 3]));
 }
 
-struct QRec {         // A2 output per query
+template <int D>
+struct QRecT {        // A2 output per query
     int valid;
     int cstar;        // kd-leaf position of the certified answer
     int id;           // centroid id (pidx[cstar])
@@ -111,50 +144,51 @@ struct QRec {         // A2 output per query
     uint32_t farmask; // far steps on c*'s root path, bit = depth
     int pad_;
     float B[16];      // suffix max of box' over far steps (certificate thresholds)
-    float o[16];      // c*'s snapshot coordinates
+    float o[D];       // c*'s snapshot coordinates
 };
 
+template <class C>
 struct Scan2Shared {
     KdTree t;
-    float dist[kMaxK];  // tree build scratch; live distances for the exact DFS
-    float rate[kMaxK];  // Single(1/sqrt(cnts[not Odd(iter)])) by kd-leaf position
+    float dist[kMaxK];     // tree build scratch; live distances for the exact DFS
+    float rate[kMaxK];     // Single(1/sqrt(cnts[not Odd(iter)])) by kd-leaf position
     float dfs_inc[kMaxK];  // exact DFS: per split node box' increment, sign = near child hi
-    alignas(16) float q[2][kBatch][16];
-    alignas(16) float qm[2][kBatch][16];  // -2 q (exact), the A1 dot-product operand
-    float cnmax[8];
-    int fxl[kBatch];   // queries of the current batch re-certified exactly    // per wave: upper bound of |c|^2 over its live centroids (monotone within a pass)
-    alignas(16) float qslow[16];       // the query resolved on its own after a failed commit
-    WaveRec wrec[8][kBatch + 1];  // column kBatch: the solo query
-    alignas(16) QRec qrec[2][kBatch];
-    QRec qsolo;
+    alignas(16) float q[2][C::KB][C::QD];
+    alignas(16) float qm[2][C::KB][C::QD];  // -2 q (exact), the A1 dot-product operand
+    float cnmax[C::NWV];   // per (virtual) wave: upper bound of |c|^2 over its live centroids (monotone within a pass)
+    int fxl[C::KB];        // queries of the current batch re-certified exactly
+    alignas(16) float qslow[C::QD];  // the query resolved on its own after a failed commit
+    WaveRecT<C::SL> wrec[C::NWV][C::KB + 1];  // column KB: the solo query
+    alignas(16) QRecT<C::D> qrec[2][C::KB];
+    QRecT<C::D> qsolo;
     // update log: entry e = wave-0 lane e (position in a VGPR, coordinates here)
-    alignas(16) float lg_c[64][kRow];
+    alignas(16) float lg_c[64][C::ROW];
     int pub_pos[64];       // log entries to fold into the registers (position, -1 = none)
-    alignas(16) float solo_c[kRow];    // coordinates of the solo query's centroid
+    alignas(16) float solo_c[C::ROW];  // coordinates of the solo query's centroid
     double err_out;
     // commit of the pending batch: versions 0..63 = log entries, 64+j = after query j
-    int vpos[kVer];
-    int vfrom[kVer];   // first query that sees the version
-    int vto[kVer];     // last query that sees it
-    alignas(16) float newc[kBatch][kRow];
-    float gp[kBatch];  // live d(q_j, c*_j)
-    int inval[kBatch];
-    int nxt[kBatch];   // next query of the batch with the same c* (kBatch = none)
-    int ient[kBatch];  // log entry holding c*_j when the commit starts (-1 = none)
-    int freel[64];     // commit: free log entries, in lane order
-    int asg[64];       // commit: log entry -> centroid position it now holds
+    int vpos[C::KVER];
+    int vfrom[C::KVER];    // first query that sees the version
+    int vto[C::KVER];      // last query that sees it
+    alignas(16) float newc[C::KB][C::ROW];
+    float gp[C::KB];       // live d(q_j, c*_j)
+    int inval[C::KB];
+    int nxt[C::KB];        // next query of the batch with the same c* (KB = none)
+    int ient[C::KB];       // log entry holding c*_j when the commit starts (-1 = none)
+    int freel[64];         // commit: free log entries, in lane order
+    int asg[64];           // commit: log entry -> centroid position it now holds
     int slow_pos;
     float slow_key;
     int any_nan;
-    int pass_done;     // end of pass: the frame converged (or hands the next pass over)
-    int st_h[16];      // exact-DFS stack (one lane)
-    float st_box[16];
-    uint32_t wkey[2][8];  // parallel exact DFS: per-wave next-improvement keys
-    alignas(16) float a2s[8][64];     // A2 scratch per wave: box terms by dimension, box' increments by depth
-    alignas(16) float a2i[8][64];
+    int pass_done;         // end of pass: the frame converged (or hands the next pass over)
+    uint32_t wkey[2][C::NWL];  // parallel exact DFS: per-wave next-improvement keys
+    alignas(16) float a2s[C::NWL][C::D > 16 ? 2 : 1][64];  // A2 scratch per wave: box terms by dimension
+    alignas(16) float a2i[C::NWL][64];                     // box' increments by depth
+    // two-CU frames: coordinates of the partner's winner per query column
+    // (this workgroup's own winner writes straight into the QRec's o[])
+    alignas(16) float lw_p[C::NWG > 1 ? C::KB + 1 : 1][C::D];
+    int xnan;              // two-CU frames: partner's NaN flag of the pass
 };
-static_assert(sizeof(Scan2Shared) <= 160 * 1024, "LDS budget (160 KB per CU)");
-static_assert(kRow >= 16 + 1, "log rows carry |c|^2 in their last float");
 
 #ifdef GSC_STAMPS
 // diagnostic build: s_memtime per pipeline phase (cdna_hip_programming.md §7)
@@ -236,43 +270,98 @@ __device__ __forceinline__ float seqdist(const float* __restrict__ a, const floa
 }
 
 // ---------------------------------------------------------------------------
-// A1: snapshot distances of one query against this wave's 512 leaves.
+// Two-CU frames: hand-offs between the two workgroups of a frame through HBM.
+// A granule is one naturally aligned 8-byte {word, tag} written by one agent-
+// scope store (write-through, single-copy atomic) and read by agent-scope
+// loads until its tag is the exchange's; tags grow by one per exchange and
+// the slots alternate by tag parity, so a slot is rewritten only after the
+// partner has read it (MI355X_MICROARCH.md, hand-off price list:
+// handoff-1to1).  Both workgroups call every exchange in the same order.
 // ---------------------------------------------------------------------------
-template <int D>
-__device__ __forceinline__ void a1_dist(const float (&creg)[8][D], const float* __restrict__ qv, float (&dv)[8]) {
+constexpr int kXCap = 2048;  // granules per slot (the DFS hands over 2048 distances)
+
+struct XPort {
+    uint64_t* mine;          // this workgroup's two slots [2][kXCap]
+    const uint64_t* theirs;  // the partner's
+    uint32_t seq;            // tag of the last exchange (uniform)
+};
+
+__device__ __forceinline__ void xput(const XPort& x, int i, uint32_t w) {
+    const uint64_t g = ((uint64_t)x.seq << 32) | w;
+    __hip_atomic_store(x.mine + (size_t)(x.seq & 1u) * kXCap + i, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t xget(const XPort& x, int i) {
+    const uint64_t* p = x.theirs + (size_t)(x.seq & 1u) * kXCap + i;
+    for (;;) {
+        const uint64_t g = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(g >> 32) == x.seq) return (uint32_t)g;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// barrier between the two workgroups of a frame that also publishes their
+// plain stores (C rows, counts) to each other: every wave drains its stores,
+// one lane releases at agent scope, swaps a granule with the partner and
+// acquires (MI355X_MICROARCH.md: valid producer / consumer forms)
+__device__ __forceinline__ void pair_barrier(XPort& x, int tid) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    ++x.seq;
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        xput(x, 0, 1u);
+        (void)xget(x, 0);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// A1: snapshot distances of one query against this wave's leaves.
+// ---------------------------------------------------------------------------
+template <int D, int SL>
+__device__ __forceinline__ void a1_dist(const float (&creg)[SL][D], const float* __restrict__ qv, float (&dv)[SL]) {
     // ANN leaf distance (ANN.dll @0x1800128b0): dist = dist + (q[d]-p[d])^2, d = 0..D-1
 #pragma unroll
-    for (int s = 0; s < 8; ++s) dv[s] = 0.0f;
+    for (int s = 0; s < SL; ++s) dv[s] = 0.0f;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         const float qd = qv[d];
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
+        for (int s = 0; s < SL; ++s) {
             const float t = fsub(qd, creg[s][d]);
             dv[s] = fadd(dv[s], fmul(t, t));
         }
     }
 }
 
-// wave min-tree over the lanes' 8 leaf distances -> the query's WaveRec
+// wave min-tree over the lanes' SL leaf distances -> the query's WaveRec
+template <int SL>
 struct A1Tree {
-    uint32_t b[8];  // this lane's leaf values (f32 bits)
+    uint32_t b[SL];  // this lane's leaf values (f32 bits)
     uint32_t lmin;
-    int sl[6];      // partner lane-group minima (order keys)
-    uint64_t m;     // lanes at the wave minimum
+    int sl[6];       // partner lane-group minima (order keys)
+    uint64_t m;      // lanes at the wave minimum
 };
 
-template <int LOGK>
-__device__ __forceinline__ A1Tree a1_tree(const float (&dv)[8], int wave, int lane) {
-    constexpr int K = 1 << LOGK;
-    const int p0 = (wave * 64 + lane) * 8;
-    A1Tree t;
-    const bool has = LOGK >= 9 || p0 < K;  // K >= 512: every lane holds 8 leaves
+template <class C>
+__device__ __forceinline__ A1Tree<C::SL> a1_tree(const float (&dv)[C::SL], int vwave, int lane) {
+    constexpr int SL = C::SL;
+    const int p0 = (vwave * 64 + lane) * SL;
+    A1Tree<SL> t;
+    const bool has = C::FULL || p0 < C::K;  // small K: only the low lanes hold leaves
 #pragma unroll
-    for (int s = 0; s < 8; ++s) t.b[s] = has ? __float_as_uint(dv[s]) : kInfBits;
-    const uint32_t m01 = fminb(t.b[0], t.b[1]), m23 = fminb(t.b[2], t.b[3]), m45 = fminb(t.b[4], t.b[5]),
-                   m67 = fminb(t.b[6], t.b[7]);
-    t.lmin = fminb(fminb(m01, m23), fminb(m45, m67));
+    for (int s = 0; s < SL; ++s) t.b[s] = has ? __float_as_uint(dv[s]) : kInfBits;
+    uint32_t mm[SL / 2];
+#pragma unroll
+    for (int s = 0; s < SL / 2; ++s) mm[s] = fminb(t.b[2 * s], t.b[2 * s + 1]);
+    if constexpr (SL == 8) {
+        t.lmin = fminb(fminb(mm[0], mm[1]), fminb(mm[2], mm[3]));
+    } else {
+        t.lmin = fminb(mm[0], mm[1]);
+    }
     // wave min-tree on order keys: partner group minima are the sibling subtrees on the path
     const int key = ordkey(t.lmin);
     int v = key;
@@ -296,7 +385,8 @@ __device__ __forceinline__ A1Tree a1_tree(const float (&dv)[8], int wave, int la
     return t;
 }
 
-__device__ __forceinline__ void a1_store(const A1Tree& t, WaveRec& rec, int lane) {
+template <int SL>
+__device__ __forceinline__ void a1_store(const A1Tree<SL>& t, WaveRecT<SL>& rec, int lane) {
     const int L = __ffsll((long long)t.m) - 1;
     if (lane == L) {
         rec.minbits = t.lmin;
@@ -304,53 +394,55 @@ __device__ __forceinline__ void a1_store(const A1Tree& t, WaveRec& rec, int lane
 #pragma unroll
         for (int i = 0; i < 6; ++i) rec.sl[i] = (uint32_t)t.sl[i];
 #pragma unroll
-        for (int s = 0; s < 8; ++s) rec.b[s] = t.b[s];
+        for (int s = 0; s < SL; ++s) rec.b[s] = t.b[s];
     }
 }
 
-template <int LOGK>
-__device__ __forceinline__ void a1_reduce(const float (&dv)[8], WaveRec& rec, int wave, int lane) {
-    a1_store(a1_tree<LOGK>(dv, wave, lane), rec, lane);
+template <class C>
+__device__ __forceinline__ void a1_reduce(const float (&dv)[C::SL], WaveRecT<C::SL>& rec, int vwave, int lane) {
+    a1_store<C::SL>(a1_tree<C>(dv, vwave, lane), rec, lane);
 }
 
 // two queries: both DPP chains are computed before either record store, so
 // their latencies overlap
-template <int LOGK>
-__device__ __forceinline__ void a1_reduce2(const float (&dv0)[8], const float (&dv1)[8], WaveRec& rec0, WaveRec& rec1,
-                                           int wave, int lane) {
-    const A1Tree t0 = a1_tree<LOGK>(dv0, wave, lane);
-    const A1Tree t1 = a1_tree<LOGK>(dv1, wave, lane);
-    a1_store(t0, rec0, lane);
-    a1_store(t1, rec1, lane);
+template <class C>
+__device__ __forceinline__ void a1_reduce2(const float (&dv0)[C::SL], const float (&dv1)[C::SL], WaveRecT<C::SL>& rec0,
+                                           WaveRecT<C::SL>& rec1, int vwave, int lane) {
+    const A1Tree<C::SL> t0 = a1_tree<C>(dv0, vwave, lane);
+    const A1Tree<C::SL> t1 = a1_tree<C>(dv1, vwave, lane);
+    a1_store<C::SL>(t0, rec0, lane);
+    a1_store<C::SL>(t1, rec1, lane);
 }
 
-template <int D, int LOGK>
-__device__ __forceinline__ void a1_query(const float (&creg)[8][D], const float* __restrict__ qv, WaveRec& rec,
-                                         int wave, int lane) {
-    float dv[8];
-    a1_dist<D>(creg, qv, dv);
-    a1_reduce<LOGK>(dv, rec, wave, lane);
+template <class C>
+__device__ __forceinline__ void a1_query(const float (&creg)[C::SL][C::D], const float* __restrict__ qv,
+                                         WaveRecT<C::SL>& rec, int vwave, int lane) {
+    float dv[C::SL];
+    a1_dist<C::D, C::SL>(creg, qv, dv);
+    a1_reduce<C>(dv, rec, vwave, lane);
 }
 
 // ---------------------------------------------------------------------------
 // A1 of the batch queries: expanded-form distance bounds instead of the exact
-// sums.  A1 keeps s~ = |c|^2 + sum_d fma(-2 q_d, c_d, .) per leaf (16 VALU ops
-// instead of 48; the wave min-tree runs in float order); A2 adds |q|^2 once.
+// sums.  A1 keeps s~ = |c|^2 + sum_d fma(-2 q_d, c_d, .) per leaf (D VALU ops
+// instead of 3D; the wave min-tree runs in float order); A2 adds |q|^2 once.
 // d~ = fl(|q|^2 + s~) differs from the reference's sequential f32 distance d
-// (ANN.dll @0x1800128b0) by at most eps(q) = (|q|^2 + M) * 2^-17, with
-// M >= |c|^2 over the live centroids: the 16 fma roundings are <= 32u(|c|^2 +
+// (ANN.dll @0x1800128b0) by at most eps(q) = (|q|^2 + M) * EPSF, with
+// M >= |c|^2 over the live centroids: the D fma roundings are <= 2D u(|c|^2 +
 // |q|^2) (every partial sum is within 2(|c|^2 + |q|^2) by Cauchy-Schwarz), the
-// two norms <= 16u each, the final add <= 2u, the reference's own sum <= 18u d
-// <= 36u(|c|^2 + |q|^2); u = 2^-24, total < 104u against the 128u used.  A2
-// certifies only with that margin; what it cannot decide is re-run exactly on
-// the same snapshot (fixup in part 2).  The committed distance g is always
-// recomputed exactly from c*'s coordinates (vp_end).
+// two norms <= D u each, the final add <= 2u, the reference's own sum <=
+// (D+1) u d <= 2(D+1) u (|c|^2 + |q|^2); u = 2^-24.  D = 16: < 104u against
+// the 128u of 2^-17; D = 32: < 200u against the 256u of 2^-16.  A2 certifies
+// only with that margin; what it cannot decide is re-run exactly on the same
+// snapshot (fixup in part 2).  The committed distance g is always recomputed
+// exactly from c*'s coordinates (vp_end).
 // ---------------------------------------------------------------------------
-template <int D>
-__device__ __forceinline__ void a1_dist_x2(const float (&creg)[8][D], const float (&cn)[8], const float* __restrict__ qm0,
-                                           const float* __restrict__ qm1, float (&dv0)[8], float (&dv1)[8]) {
+template <int D, int SL>
+__device__ __forceinline__ void a1_dist_x2(const float (&creg)[SL][D], const float (&cn)[SL],
+                                           const float* __restrict__ qm0, const float* __restrict__ qm1,
+                                           float (&dv0)[SL], float (&dv1)[SL]) {
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
+    for (int s = 0; s < SL; ++s) {
         dv0[s] = cn[s];
         dv1[s] = cn[s];
     }
@@ -358,7 +450,7 @@ __device__ __forceinline__ void a1_dist_x2(const float (&creg)[8][D], const floa
     for (int d = 0; d < D; ++d) {
         const float m0 = qm0[d], m1 = qm1[d];
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
+        for (int s = 0; s < SL; ++s) {
             dv0[s] = __builtin_fmaf(m0, creg[s][d], dv0[s]);
             dv1[s] = __builtin_fmaf(m1, creg[s][d], dv1[s]);
         }
@@ -395,9 +487,9 @@ __device__ __forceinline__ float fsum16(float v) {  // sum over each aligned 16-
 // ---------------------------------------------------------------------------
 // A2: certificates of 4 queries per wave (16 lanes per query, lane = depth).
 // ---------------------------------------------------------------------------
-template <int D, int LOGK, int NW, bool APPROX>
-__device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const float (*qrows)[16], QRec* recs, int wcol0,
-                                         const int* jlist, int lane
+template <class C, bool APPROX>
+__device__ __forceinline__ void a2_group(Scan2Shared<C>& sh, int j0, int nq, const float (*qrows)[C::QD],
+                                         QRecT<C::D>* recs, int wcol0, const int* jlist, int lane
 #ifdef GSC_STAMPS
                                          , uint64_t* acc = nullptr, uint64_t* tl = nullptr
 #endif
@@ -412,7 +504,8 @@ __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const 
 #else
 #define ASTAMP(k)
 #endif
-    constexpr int KW = LOGK >= 9 ? LOGK - 9 : 0;  // depths resolved at wave level
+    constexpr int D = C::D, LOGK = C::LOGK, NW = C::NWV, SL = C::SL, LS = C::LS;
+    constexpr int KW = C::KW;  // depths resolved at wave level
     const int l = lane & 15, gbase = lane & ~15;
     const int t = j0 + (lane >> 4);  // query slot (an index into jlist when given)
     const bool qa = t < nq;
@@ -426,10 +519,10 @@ __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const 
     const uint32_t nmin = sum16((mw == gmin && l < NW) ? 1u : 0u);
     const int W = (int)min16((mw == gmin && l < NW) ? (uint32_t)l : 99u);
     const int Wv = W < NW ? W : 0;
-    const WaveRec& r = sh.wrec[Wv][wc];
+    const WaveRecT<SL>& r = sh.wrec[Wv][wc];
     bool tie2;
-    const int ls = rec_slot(r, &tie2);
-    const int cstar = (Wv * 64 + (r.lanebits & 255)) * 8 + ls;
+    const int ls = rec_slot<SL>(r, &tie2);
+    const int cstar = (Wv * 64 + (r.lanebits & 255)) * SL + ls;
     const bool tie = nmin > 1 || tie2;
     const float* q = qrows[jr];
     ASTAMP(12)
@@ -442,8 +535,10 @@ __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const 
         for (int w = 0; w < NW; ++w)
             if ((w >> sh_) == want) sib = fminb(sib, sh.wrec[w][wc].minbits);
     } else if (l < LOGK) {
-        const int idx = l <= LOGK - 4 ? (LOGK - 4 - l) : (l == LOGK - 3 ? 8 : (l == LOGK - 2 ? 7 : 6));
-        sib = rec_sib(r, ls, idx);
+        // lane levels: depths [KW, LOGK - LS) -> sibling lane groups 5..0;
+        // slot levels: depths [LOGK - LS, LOGK) -> 8 (quad), 7 (pair), 6 (slot)
+        const int idx = l < LOGK - LS ? (LOGK - LS - 1 - l) : (6 + (LOGK - 1 - l));
+        sib = rec_sib<SL>(r, ls, idx);
     }
     // split node at depth l on c*'s root path (ANNkd_split::ann_search)
     bool far = false;
@@ -464,26 +559,31 @@ __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const 
     }
     const uint32_t farmask = (uint32_t)(__ballot(far) >> gbase) & 0xFFFFu;
     ASTAMP(13)
-    // annBoxDistance(q, enclosing rect): lane l holds dimension l's term (or
-    // -1 = inside), summed below in dimension order; box' increments by depth
+    // annBoxDistance(q, enclosing rect): lane l holds dimension l's term (and
+    // l + 16's at D = 32; -1 = inside), summed below in dimension order; box'
+    // increments by depth
+    constexpr int NH = D > 16 ? 2 : 1;
     {
-        float term = -1.0f;
-        if (l < D) {
-            const float qd = q[l], blo = sh.t.bnd_lo[l], bhi = sh.t.bnd_hi[l];
-            const bool below = blo > qd, above = qd > bhi;
-            const float t = below ? fsub(blo, qd) : fsub(qd, bhi);
-            term = (below || above) ? fmul(t, t) : -1.0f;
+#pragma unroll
+        for (int hh = 0; hh < NH; ++hh) {
+            const int dd = l + 16 * hh;
+            float term = -1.0f;
+            if (dd < D) {
+                const float qd = q[dd], blo = sh.t.bnd_lo[dd], bhi = sh.t.bnd_hi[dd];
+                const bool below = blo > qd, above = qd > bhi;
+                const float tt = below ? fsub(blo, qd) : fsub(qd, bhi);
+                term = (below || above) ? fmul(tt, tt) : -1.0f;
+            }
+            sh.a2s[wave_of_lane()][hh][lane] = term;
         }
-        sh.a2s[wave_of_lane()][lane] = term;
         sh.a2i[wave_of_lane()][lane] = inc;
     }
     wave_lds_sync();
     float box = 0.0f;
     {
-        const float* tv = &sh.a2s[wave_of_lane()][gbase];
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            const float v = tv[d];
+            const float v = sh.a2s[wave_of_lane()][d >> 4][gbase + (d & 15)];
             box = v >= 0.0f ? fadd(box, v) : box;
         }
     }
@@ -513,11 +613,12 @@ __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const 
     if constexpr (APPROX) {
         // A1 values are within eps of the reference's distances: certify with margins
         const float qs = l < D ? q[l] : 0.0f;
-        const float qn = fsum16(__builtin_fmaf(qs, qs, 0.0f));
+        const float qs2 = (D > 16 && l + 16 < D) ? q[l + 16] : 0.0f;
+        const float qn = fsum16(__builtin_fmaf(qs2, qs2, __builtin_fmaf(qs, qs, 0.0f)));
         float M = 0.0f;
 #pragma unroll
         for (int w = 0; w < NW; ++w) M = fmaxf(M, sh.cnmax[w]);
-        const float eps = fadd(fmul(fadd(qn, M), 0x1p-17f), 1e-37f);
+        const float eps = fadd(fmul(fadd(qn, M), C::EPSF), 1e-37f);
         ok = !far || (fsub(fadd(qn, __uint_as_float(sib)), eps) > Bv);
         unique = fsub(__uint_as_float(m2), __uint_as_float(gmin)) > fadd(eps, eps);
         m2lo = fsub(fadd(qn, __uint_as_float(m2)), eps);
@@ -529,7 +630,7 @@ __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const 
     const bool gok = ((__ballot(!ok) >> gbase) & 0xFFFFull) == 0;
     const bool valid = unique && __uint_as_float(gmin) <= FLT_MAX && gok;
     if (qa) {
-        QRec& R = recs[jj];
+        QRecT<D>& R = recs[jj];
         if (l < LOGK) R.B[l] = Bv;
         if (l == 0) {
             R.valid = valid ? 1 : 0;
@@ -542,6 +643,7 @@ __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const 
         }
     }
     ASTAMP(15)
+    (void)LS;
 }
 #undef ASTAMP
 
@@ -549,7 +651,7 @@ __device__ __forceinline__ void a2_group(Scan2Shared& sh, int j0, int nq, const 
 // Commit, step 1 (wave 0, lanes = queries j of the pending batch): online
 // updates in order per centroid (encoder.lpr:735-740, f32 c += (x - c) * rate)
 // assuming every query of the batch commits; version table for the checks.
-// Log entry e is lane e: position lg_pos (-1 = empty), tag = committing batch.
+// Log entry e is lane e: position lg_pos (-1 = empty), tag = commit iteration.
 // ---------------------------------------------------------------------------
 // Scan state of one pending query (lane j) / log entry (lane e), built one
 // step per A1 query so the LDS round trips hide under wave 0's distance work.
@@ -557,14 +659,14 @@ struct VPState {
     int cs, pred, nxt, first, ie;
 };
 
-template <int D, int LOGK>
-__device__ __forceinline__ void vp_begin(Scan2Shared& sh, int qb, int off, int pn, int a1, int lane, int& lg_pos,
+template <class C>
+__device__ __forceinline__ void vp_begin(Scan2Shared<C>& sh, int qb, int off, int pn, int a1, int lane, int& lg_pos,
                                          int lg_tag, VPState& st) {
     if (lg_pos >= 0 && lg_tag < a1) lg_pos = -1;  // committed before the batch's snapshot
     st.cs = lane < pn ? sh.qrec[qb][off + lane].cstar : -2;
     st.pred = -1;
-    st.nxt = kBatch;
-    st.first = kBatch;
+    st.nxt = C::KB;
+    st.first = C::KB;
     st.ie = 64;
     sh.vpos[lane] = lg_pos;
     sh.vfrom[lane] = 0;
@@ -573,32 +675,30 @@ __device__ __forceinline__ void vp_begin(Scan2Shared& sh, int qb, int off, int p
 
 // step k (uniform): pending query k against every lane's query / entry, all
 // in registers (c*_k by readlane, the entries holding it by ballot)
+template <class C>
 __device__ __forceinline__ void vp_step(int k, int lane, int lg_pos, VPState& st) {
     const int ck = __builtin_amdgcn_readlane(st.cs, k);  // -2 past the batch: matches nothing
     const bool same = ck == st.cs;
     if (k < lane && same) st.pred = 64 + k;
-    if (k > lane && same && st.nxt == kBatch) st.nxt = k;
-    if (ck == lg_pos && st.first == kBatch) st.first = k;  // lane as log entry: first query moving it
+    if (k > lane && same && st.nxt == C::KB) st.nxt = k;
+    if (ck == lg_pos && st.first == C::KB) st.first = k;  // lane as log entry: first query moving it
     const uint64_t em = __ballot(lg_pos == ck);            // entries holding c*_k (lowest = ie_k)
     if (lane == k && em) st.ie = __ffsll((long long)em) - 1;
 }
 
-// Commit, step 1 (wave 0, lanes = queries j of the pending batch): online
-// updates in order per centroid (encoder.lpr:735-740, f32 c += (x - c) * rate)
-// assuming every query of the batch commits; version table for the checks.
-// Log entry e is lane e: position lg_pos (-1 = empty), tag = commit iteration.
-template <int D, int LOGK>
-__device__ __forceinline__ void vp_end(Scan2Shared& sh, int qb, int off, int pn, int lane, int lg_pos,
+template <class C>
+__device__ __forceinline__ void vp_end(Scan2Shared<C>& sh, int qb, int off, int pn, int lane, int lg_pos,
                                        const VPState& st) {
+    constexpr int D = C::D, KB = C::KB;
     const int j = lane;
     const bool act = j < pn;
-    const QRec& R = sh.qrec[qb][off + (act ? j : 0)];
+    const QRecT<D>& R = sh.qrec[qb][off + (act ? j : 0)];
     const int cs = st.cs, nxt = st.nxt;
     const int ie = st.ie < 64 ? st.ie : -1;  // log entry holding c*_j (c*_j moved before the batch)
     const int pred = st.pred >= 0 ? st.pred : ie;
     // versions: log entries (0..63) and "after query j" (64+j)
     sh.vto[lane] = lg_pos >= 0 ? st.first : -1;
-    if (lane < kBatch) {
+    if (lane < KB) {
         sh.vpos[64 + lane] = act ? cs : -1;
         sh.vfrom[64 + lane] = j + 1;
         sh.vto[64 + lane] = act ? nxt : -1;
@@ -635,15 +735,16 @@ __device__ __forceinline__ void vp_end(Scan2Shared& sh, int qb, int off, int pn,
 
 // Commit, step 2 (all threads): every (query, moved centroid) pair of the
 // pending batch -- the moved centroid must stay provably outside ANN's answer.
-// Lane = query j (lane & 31); wave / half-wave = a strided share of the
-// versions, so each version row is one LDS broadcast per half-wave and the
-// query row stays in registers.
-template <int D, int LOGK, int NW>
-__device__ __forceinline__ void v_check_q(Scan2Shared& sh, int qb, int off, int pn, int wave, int lane) {
-    const int j = lane & 31, hf = lane >> 5;
+// Lane = query j (lane % KB); wave / lane group = a strided share of the
+// versions, so each version row is one LDS broadcast per group and the query
+// row stays in registers.  (Both workgroups of a two-CU frame check every pair.)
+template <class C>
+__device__ __forceinline__ void v_check_q(Scan2Shared<C>& sh, int qb, int off, int pn, int wave, int lane) {
+    constexpr int D = C::D, KB = C::KB, QPL = 64 / KB, LOGK = C::LOGK;
+    const int j = lane % KB, grp = lane / KB;
     const bool act = j < pn;
     const int jr = act ? j : 0;
-    const QRec& R = sh.qrec[qb][off + jr];
+    const QRecT<D>& R = sh.qrec[qb][off + jr];
     const int cs = R.cstar;
     const uint32_t fm = R.farmask;
     const float g = sh.gp[jr];
@@ -652,7 +753,7 @@ __device__ __forceinline__ void v_check_q(Scan2Shared& sh, int qb, int off, int 
     for (int d = 0; d < D; ++d) q[d] = sh.q[qb][off + jr][d];
     bool bad = false;
 #pragma unroll 1
-    for (int v = wave * 2 + hf; v < kVer; v += 2 * NW) {
+    for (int v = wave * QPL + grp; v < C::KVER; v += QPL * C::NWL) {
         const int vp = sh.vpos[v];
         if (vp < 0 || !act || j < sh.vfrom[v] || j > sh.vto[v] || vp == cs) continue;
         const float* c = v < 64 ? sh.lg_c[v] : sh.newc[v - 64];
@@ -669,102 +770,6 @@ __device__ __forceinline__ void v_check_q(Scan2Shared& sh, int qb, int off, int 
     if (bad) sh.inval[j] = 1;
 }
 
-template <int D, int LOGK>
-__device__ __forceinline__ void v_check(Scan2Shared& sh, int qb, int off, int pn, int tid, int nthreads) {
-    const int npairs = pn * kVer;
-    for (int p = tid; p < npairs; p += nthreads) {
-        const int j = p / kVer, v = p - j * kVer;
-        const int vp = sh.vpos[v];
-        if (vp < 0 || j < sh.vfrom[v] || j > sh.vto[v]) continue;
-        const QRec& R = sh.qrec[qb][off + j];
-        const int cs = R.cstar;
-        if (vp == cs) continue;  // c* itself: checked in v_prepare
-        const float* c = v < 64 ? sh.lg_c[v] : sh.newc[v - 64];
-        const float du = seqdist<D>(sh.q[qb][off + j], c);
-        const float g = sh.gp[j];
-        const int lca = __clz(vp ^ cs) - (32 - LOGK);
-        const bool farl = (R.farmask >> lca) & 1u;
-        if (!(du > g && (!farl || du > R.B[lca]))) sh.inval[j] = 1;
-    }
-}
-
-// Exact ANN ann_search (k = 1, eps = 0; annkSearch @0x1800124b0) over the
-// stale tree with the live leaf distances in sh.dist -- one lane, stack in
-// LDS.  No NaN distances reach this kernel (those passes run the generic
-// kernel), so leaf early exits cannot change a result.
-// Exact ANN ann_search (k = 1, eps = 0; annkSearch @0x1800124b0) over the
-// stale tree with the live leaf distances in sh.dist, for the query in
-// sh.qslow.  All threads first tabulate every split node's near child and
-// box' increment (ANNkd_split::ann_search: cut = q[cd] - cv; bd = lo - q[cd]
-// or q[cd] - hi, clamped at 0; box' = (cut^2 - bd^2) + box), then one lane
-// walks the DFS with the stack in LDS.  No NaN distances reach this kernel
-// (those passes run the generic kernel), so leaf early exits cannot change a
-// result.
-template <int D, int LOGK>
-__device__ __forceinline__ void dfs_exact(Scan2Shared& sh, int tid, int nthreads) {
-    constexpr int K = 1 << LOGK;
-    const float* q = sh.qslow;
-    for (int h = tid; h < K - 1; h += nthreads) {
-        const int cdim = sh.t.cd[h];
-        const float qc = q[cdim];
-        const float cut = fsub(qc, sh.t.cv[h]);
-        const bool nearlo = cut < 0.0f;
-        float bd = nearlo ? fsub(sh.t.lo[h], qc) : fsub(qc, sh.t.hi[h]);
-        if (bd < 0.0f) bd = 0.0f;
-        const float inc = fsub(fmul(cut, cut), fmul(bd, bd));  // >= +0
-        sh.dfs_inc[h] = nearlo ? inc : -inc;
-    }
-    lds_barrier();
-    if (tid == 0) {
-        float cur_box = 0.0f;
-        for (int d = 0; d < D; ++d) {  // annBoxDistance
-            const float qd = q[d];
-            if (sh.t.bnd_lo[d] > qd) {
-                const float t = fsub(sh.t.bnd_lo[d], qd);
-                cur_box = fadd(cur_box, fmul(t, t));
-            } else if (qd > sh.t.bnd_hi[d]) {
-                const float t = fsub(qd, sh.t.bnd_hi[d]);
-                cur_box = fadd(cur_box, fmul(t, t));
-            }
-        }
-        int h = 0, sp = 0, best = -1;
-        float key = FLT_MAX;
-        for (;;) {
-            if (h >= K - 1) {
-                // ANNkd_leaf::ann_search: insert iff the list is empty or key > dist
-                const int p = h - (K - 1);
-                const float dd = sh.dist[p];
-                if (best < 0 || key > dd) {
-                    key = dd;
-                    best = p;
-                }
-                // unwind: the far child is visited iff box' < max_key
-                bool found = false;
-                while (sp > 0) {
-                    --sp;
-                    if (sh.st_box[sp] < key) {
-                        h = sh.st_h[sp];
-                        cur_box = sh.st_box[sp];
-                        found = true;
-                        break;
-                    }
-                }
-                if (!found) break;
-                continue;
-            }
-            const float v = sh.dfs_inc[h];
-            const int hi = __float_as_uint(v) >> 31;
-            sh.st_box[sp] = fadd(cur_box, fabsf(v));
-            sh.st_h[sp] = 2 * h + 2 - hi;
-            ++sp;
-            h = 2 * h + 1 + hi;
-        }
-        sh.slow_pos = best;
-        sh.slow_key = key;
-    }
-    lds_barrier();
-}
-
 // Exact ANN ann_search (k = 1, eps = 0; annkSearch @0x1800124b0), all
 // threads: the result of the stale-tree DFS is decided by its strict
 // improvements only.  With leaves ranked in near-first DFS order, a leaf is
@@ -773,9 +778,12 @@ __device__ __forceinline__ void dfs_exact(Scan2Shared& sh, int tid, int nthreads
 // along a path, so that is one test on its innermost far subtree (start rank
 // s*, box' bx*).  The next improvement is the lowest-ranked reached leaf with
 // d < b, found by one block min-reduction per improvement.  Live leaf
-// distances come from sh.dist.
-template <int D, int LOGK, int NW>
-__device__ __forceinline__ void dfs_parallel(Scan2Shared& sh, int tid, int lane, int wave, int& out_pos, float& out_key) {
+// distances come from sh.dist.  No NaN distances reach this kernel (those
+// passes run the generic kernel), so leaf early exits cannot change a result.
+template <class C>
+__device__ __forceinline__ void dfs_parallel(Scan2Shared<C>& sh, int tid, int lane, int wave, int& out_pos,
+                                             float& out_key) {
+    constexpr int D = C::D, LOGK = C::LOGK, NW = C::NWL;
     constexpr int K = 1 << LOGK;
     constexpr int nthreads = 64 * NW;
     const float* q = sh.qslow;
@@ -802,7 +810,7 @@ __device__ __forceinline__ void dfs_parallel(Scan2Shared& sh, int tid, int lane,
         }
     }
     lds_barrier();
-    // this lane's 8 leaves (an aligned depth LOGK-3 subtree): DFS rank, start
+    // this thread's 8 leaves (an aligned depth LOGK-3 subtree): DFS rank, start
     // rank and box' of the innermost far subtree (-1 / none if all-near)
     const int p0 = tid * 8;
     int rs[8];  // rank << 13 | (s* + 1)
@@ -875,22 +883,23 @@ __device__ __forceinline__ void dfs_parallel(Scan2Shared& sh, int tid, int lane,
 }
 
 // fold published log entries into the owners' registers
-template <int D>
-__device__ __forceinline__ void refresh(Scan2Shared& sh, float (&creg)[8][D], float (&cn)[8], float& cnmax, int wave,
-                                        int lane) {
+template <class C>
+__device__ __forceinline__ void refresh(Scan2Shared<C>& sh, float (&creg)[C::SL][C::D], float (&cn)[C::SL],
+                                        float& cnmax, int vwave, int lane) {
+    constexpr int SL = C::SL, LS = C::LS, D = C::D;
     const int pp = sh.pub_pos[lane];
-    uint64_t m = __ballot(pp >= 0 && (pp >> 9) == wave);
+    uint64_t m = __ballot(pp >= 0 && (pp >> (6 + LS)) == vwave);
     const bool any = m != 0;
     while (m) {
         const int e = __ffsll((long long)m) - 1;
         m &= m - 1;
         const int p = __builtin_amdgcn_readlane(pp, e);
-        const int owner = (p >> 3) & 63, slot = p & 7;
-        const float nv = sh.lg_c[e][kRow - 1];  // |c|^2, written with the entry
+        const int owner = (p >> LS) & 63, slot = p & (SL - 1);
+        const float nv = sh.lg_c[e][C::ROW - 1];  // |c|^2, written with the entry
         // the wave's norm bound only grows within a pass (A2 reads it for any earlier snapshot)
         cnmax = fmaxf(cnmax, nv);
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
+        for (int s = 0; s < SL; ++s) {
             if (s == slot) {
 #pragma unroll
                 for (int d = 0; d < D; ++d) {
@@ -901,14 +910,17 @@ __device__ __forceinline__ void refresh(Scan2Shared& sh, float (&creg)[8][D], fl
             }
         }
     }
-    if (any && lane == 0) sh.cnmax[wave] = cnmax;
+    if (any && lane == 0) sh.cnmax[vwave] = cnmax;
 }
 
-// c*'s snapshot coordinates for the queries in qmask of batch buffer buf, written by the lane that owns c*
-// (the first wave / lane / slot at the minimum of the A1 records, as in A2)
-template <int D, int NW>
-__device__ __forceinline__ void write_cstar(Scan2Shared& sh, const float (&creg)[8][D], int buf, uint64_t qmask,
-                                            int wave, int lane) {
+// c*'s snapshot coordinates for the queries in qmask (columns col0 + j),
+// written by the lane that owns c* (the first wave / lane / slot at the
+// minimum of the A1 records, as in A2) -- over this workgroup's waves only --
+// into recs[j].o
+template <class C>
+__device__ __forceinline__ void write_cstar(Scan2Shared<C>& sh, const float (&creg)[C::SL][C::D], QRecT<C::D>* recs,
+                                            uint64_t qmask, int col0, int wave, int lane, int wg) {
+    constexpr int SL = C::SL, D = C::D, NWL = C::NWL;
     uint64_t won;
     {
         const bool act = (qmask >> lane) & 1ull;
@@ -916,8 +928,8 @@ __device__ __forceinline__ void write_cstar(Scan2Shared& sh, const float (&creg)
         float gm = __builtin_inff();
         int W = 0;
 #pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            const float m = __uint_as_float(sh.wrec[w][jq].minbits);
+        for (int w = 0; w < NWL; ++w) {
+            const float m = __uint_as_float(sh.wrec[wg * NWL + w][col0 + jq].minbits);
             if (m < gm) {
                 gm = m;
                 W = w;
@@ -928,40 +940,158 @@ __device__ __forceinline__ void write_cstar(Scan2Shared& sh, const float (&creg)
     while (won) {
         const int jj = __ffsll((long long)won) - 1;
         won &= won - 1;
-        const WaveRec& r = sh.wrec[wave][jj];
+        const WaveRecT<SL>& r = sh.wrec[wg * NWL + wave][col0 + jj];
         bool tie2;
-        const int owner = r.lanebits & 255, slot = rec_slot(r, &tie2);
+        const int owner = r.lanebits & 255, slot = rec_slot<SL>(r, &tie2);
+        float* dst = recs[jj].o;
 #pragma unroll
-        for (int s = 0; s < 8; ++s)
+        for (int s = 0; s < SL; ++s)
             if (s == slot && lane == owner) {
 #pragma unroll
-                for (int d = 0; d < D; ++d) sh.qrec[buf][jj].o[d] = creg[s][d];
+                for (int d = 0; d < D; ++d) dst[d] = creg[s][d];
             }
     }
 }
 
-template <int D, int LOGK>
-__global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict__ frames, int nframes,
-                                                         const float* __restrict__ Xall, float* __restrict__ Call,
-                                                         int* __restrict__ i_scratch, const float* __restrict__ rate_tab,
-                                                         double tol, int max_passes) {
-    constexpr int K = 1 << LOGK;
-    constexpr int NW = K >= 512 ? K / 512 : 1;
-    constexpr int kErrWave = NW > 1 ? 1 : 0;  // residual + cluster ids (wave 0 keeps the log)
+// ---- two-CU frames: the exchanges ------------------------------------------
+// this workgroup's winner wave of a column (first at the minimum, as write_cstar)
+template <class C>
+__device__ __forceinline__ int local_winner(const Scan2Shared<C>& sh, int col, int base) {
+    float gm = __builtin_inff();
+    int W = 0;
+#pragma unroll
+    for (int w = 0; w < C::NWL; ++w) {
+        const float m = __uint_as_float(sh.wrec[base + w][col].minbits);
+        if (m < gm) {
+            gm = m;
+            W = w;
+        }
+    }
+    return W;
+}
+
+// A1 records: per query column, the 8 wave minima of this workgroup, its
+// winning wave's whole record and that winner's coordinates; then the 8 wave
+// norm bounds.  The partner's values land in the partner's virtual rows.
+template <class C>
+__device__ __forceinline__ void xchg_records(Scan2Shared<C>& sh, XPort& x, int nq, const int* cols, int col0,
+                                             const QRecT<C::D>* recs, int tid, int wg) {
+    constexpr int D = C::D, NWL = C::NWL, RW = (int)(sizeof(WaveRecT<C::SL>) / 4);
+    constexpr int PQ = NWL + 1 + RW + D;  // words per query
+    const int nw = nq * PQ + NWL;
+    ++x.seq;
+    const int mine0 = wg * NWL, their0 = (1 - wg) * NWL;
+    for (int i = tid; i < nw; i += C::NT) {
+        uint32_t w;
+        if (i < nq * PQ) {
+            const int jq = i / PQ, f = i - jq * PQ;
+            const int col = cols ? col0 + cols[jq] : col0 + jq;
+            if (f < NWL) {
+                w = sh.wrec[mine0 + f][col].minbits;
+            } else if (f == NWL) {
+                w = (uint32_t)local_winner<C>(sh, col, mine0);
+            } else if (f < NWL + 1 + RW) {
+                const int W = local_winner<C>(sh, col, mine0);
+                w = reinterpret_cast<const uint32_t*>(&sh.wrec[mine0 + W][col])[f - NWL - 1];
+            } else {
+                w = __float_as_uint(recs[col - col0].o[f - NWL - 1 - RW]);
+            }
+        } else {
+            w = __float_as_uint(sh.cnmax[mine0 + (i - nq * PQ)]);
+        }
+        xput(x, i, w);
+    }
+    for (int i = tid; i < nw; i += C::NT) {
+        if (i < nq * PQ) {
+            const int jq = i / PQ, f = i - jq * PQ;
+            const int col = cols ? col0 + cols[jq] : col0 + jq;
+            if (f < NWL) {
+                sh.wrec[their0 + f][col].minbits = xget(x, i);
+            } else if (f == NWL) {
+                (void)xget(x, i);
+            } else if (f < NWL + 1 + RW) {
+                const int W = (int)xget(x, jq * PQ + NWL);
+                const uint32_t v = xget(x, i);
+                if (f - NWL - 1 != 0)  // the minbits word is written by the f < NWL branch
+                    reinterpret_cast<uint32_t*>(&sh.wrec[their0 + W][col])[f - NWL - 1] = v;
+            } else {
+                sh.lw_p[col][f - NWL - 1 - RW] = __uint_as_float(xget(x, i));
+            }
+        } else {
+            sh.cnmax[their0 + (i - nq * PQ)] = __uint_as_float(xget(x, i));
+        }
+    }
+}
+
+// after xchg_records: the partner's winner coordinates into o[] of the listed
+// columns where the partner holds the global winner (the lower virtual waves
+// win ties: workgroup 0)
+template <class C>
+__device__ __forceinline__ void fill_winner_coords(Scan2Shared<C>& sh, QRecT<C::D>* recs, int nq, const int* cols,
+                                                   int col0, int tid, int wg) {
+    constexpr int D = C::D, NWL = C::NWL;
+    for (int i = tid; i < nq * D; i += C::NT) {
+        const int jq = i / D, d = i - jq * D;
+        const int j = cols ? cols[jq] : jq;
+        float m0 = __builtin_inff(), m1 = __builtin_inff();
+#pragma unroll
+        for (int w = 0; w < NWL; ++w) {
+            m0 = fminf(m0, __uint_as_float(sh.wrec[w][col0 + j].minbits));
+            m1 = fminf(m1, __uint_as_float(sh.wrec[NWL + w][col0 + j].minbits));
+        }
+        const int gw = m1 < m0 ? 1 : 0;
+        if (gw != wg) recs[j].o[d] = sh.lw_p[col0 + j][d];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The kernel.  NWG = 1: one workgroup per frame (blockIdx.x = frame).
+// NWG = 2: a cooperative grid of frame pairs; workgroups 2p / 2p + 1 (by
+// default; b and b + 8 when the grid is a multiple of 16, so a pair shares
+// an XCD's L2) run frames p, p + npairs, ...
+// ---------------------------------------------------------------------------
+template <class C>
+__global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restrict__ frames, int nframes,
+                                                           const float* __restrict__ Xall, float* __restrict__ Call,
+                                                           int* __restrict__ i_scratch,
+                                                           const float* __restrict__ rate_tab, double tol,
+                                                           int max_passes, uint64_t* __restrict__ xbuf) {
+    constexpr int D = C::D, K = C::K, SL = C::SL, LS = C::LS, NWL = C::NWL, KB = C::KB, NWG = C::NWG;
+    constexpr int kErrWave = NWL > 1 ? 1 : 0;  // residual + cluster ids (wave 0 keeps the log)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    Scan2Shared& sh = *reinterpret_cast<Scan2Shared*>(smem);
-    const int fi = blockIdx.x;
-    if (fi >= nframes) return;
+    Scan2Shared<C>& sh = *reinterpret_cast<Scan2Shared<C>*>(smem);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int nthreads = C::NT;
+    int wg = 0, fi0 = blockIdx.x, fstep = nframes;
+    if constexpr (NWG == 2) {
+        const int nb = gridDim.x, b = blockIdx.x;
+        if (nb % 16 == 0) {
+            wg = (b >> 3) & 1;
+            fi0 = (b >> 4) * 8 + (b & 7);
+        } else {
+            wg = b & 1;
+            fi0 = b >> 1;
+        }
+        fstep = nb / 2;
+    }
+    const int vwave = wg * NWL + wave;  // this wave's virtual index
+    const bool wg0 = wg == 0;
+    for (int fi = fi0; fi < nframes; fi += fstep) {
     ReduceFrame* frp = frames + fi;
-    if (uniform_int(frp->done)) return;
+    if (uniform_int(frp->done) || uniform_int(frp->generic)) continue;
     const int N = uniform_int(frp->N);
     const float* __restrict__ X = uniform_ptr(Xall + frp->x_off);
-    float* C = uniform_ptr(Call + frp->c_off);
+    float* C_ = uniform_ptr(Call + frp->c_off);
     int* clusters = uniform_ptr(i_scratch + frp->n_off);
     int* prev_cnt = uniform_ptr(i_scratch + frp->k_off);  // cnts[not Odd(iter)] by centroid id
     int* cnta = uniform_ptr(i_scratch + frp->ka_off);     // cnts[Odd(iter)] by kd-leaf position
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int nthreads = 64 * NW;
+    XPort xp{nullptr, nullptr, 0};
+    if constexpr (NWG == 2) {
+        xp.mine = xbuf + ((size_t)fi * 2 + wg) * 2 * kXCap;
+        xp.theirs = xbuf + ((size_t)fi * 2 + (1 - wg)) * 2 * kXCap;
+        xp.seq = (uint32_t)uniform_int(frp->xseq);
+    }
+    double prev_err = uniform_int(frp->iters) == 0 ? 3.4028234663852886e+38 : frp->err;  // err := MaxSingle
 
     // All of the frame's passes run in this launch (the pass index lives in
     // the frame descriptor), so a frame never waits for the slowest frame of a
@@ -970,65 +1100,85 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
 #ifdef GSC_STAMPS
     const uint64_t t_kernel0 = stamp();
 #endif
-    if (pass == 0)
+    if (pass == 0 && wg0)
         for (int k = tid; k < K; k += nthreads) prev_cnt[k] = 1;  // CCntStart (encoder.lpr:717-721)
     if (tid == 0) sh.any_nan = 0;
+    if constexpr (NWG == 2) {
+        if (pass == 0) pair_barrier(xp, tid);  // workgroup 1 reads prev_cnt below: workgroup 0 wrote it
+    }
     __syncthreads();
-    if (!build_tree_fast<D, LOGK, 64 * NW>(sh.t, sh.dist, sh.dfs_inc, C, &sh.slow_pos)) {
-        build_tree<D>(sh.t, sh.dist, C, K);  // median ties: quickselect's exact order
-        if (tid == 0) frp->tree_exact += 1;
+    if (!build_tree_fast<D, C::LOGK, nthreads>(sh.t, sh.dist, sh.dfs_inc, C_, &sh.slow_pos)) {
+        build_tree<D>(sh.t, sh.dist, C_, K);  // median ties: quickselect's exact order
+        if (tid == 0 && wg0) frp->tree_exact += 1;
     }
 
-    float creg[8][D];
-    float cn[8];  // |c|^2 per register leaf (A1 bounds)
-    const int p0 = tid * 8;
+    float creg[SL][D];
+    float cn[SL];  // |c|^2 per register leaf (A1 bounds)
+    const int p0 = (vwave * 64 + lane) * SL;
     bool nan_here = false;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
+    for (int s = 0; s < SL; ++s) {
         const int p = p0 + s;
         if (p < K) {
             const int id = sh.t.pidx[p];
 #pragma unroll
             for (int d = 0; d < D; ++d) {
-                creg[s][d] = C[(int64_t)id * D + d];
+                creg[s][d] = C_[(int64_t)id * D + d];
                 nan_here |= creg[s][d] != creg[s][d];
             }
-            sh.rate[p] = rate_tab[prev_cnt[id]];
-            cnta[p] = 1;
         } else {
 #pragma unroll
             for (int d = 0; d < D; ++d) creg[s][d] = 0.0f;
         }
         cn[s] = norm2_x<D>(creg[s]);
     }
+    // rates of every position (both workgroups of a two-CU frame commit any c*)
+    for (int p = tid; p < K; p += nthreads) {
+        sh.rate[p] = rate_tab[prev_cnt[sh.t.pidx[p]]];  // Single(1/sqrt(cnts[not Odd(iter)]))
+        if (wg0) cnta[p] = 1;
+    }
     if (nan_here) sh.any_nan = 1;
     float cnmax;
     {
         float mx = 0.0f;
 #pragma unroll
-        for (int s = 0; s < 8; ++s) mx = fmaxf(mx, cn[s]);
+        for (int s = 0; s < SL; ++s) mx = fmaxf(mx, cn[s]);
         cnmax = wave_max_nonneg(nan_here ? 0.0f : mx);  // NaN passes leave for the generic kernel below
-        if (lane == 0) sh.cnmax[wave] = cnmax;
+        if (lane == 0) sh.cnmax[vwave] = cnmax;
     }
     // first batch's queries
-    const int n0 = min(kBatch, N);
+    const int n0 = min(KB, N);
     for (int k = tid; k < n0 * D; k += nthreads) {
         const float x = X[k];
         sh.q[0][k / D][k % D] = x;
         sh.qm[0][k / D][k % D] = -2.0f * x;
     }
     __syncthreads();
+    if constexpr (NWG == 2) {  // agree on NaN and share the wave norm bounds
+        ++xp.seq;
+        if (tid < NWL) xput(xp, tid, __float_as_uint(sh.cnmax[wg * NWL + tid]));
+        if (tid == NWL) xput(xp, NWL, (uint32_t)sh.any_nan);
+        if (tid < NWL) sh.cnmax[(1 - wg) * NWL + tid] = __uint_as_float(xget(xp, tid));
+        if (tid == NWL) sh.xnan = (int)xget(xp, NWL);
+        __syncthreads();
+        if (tid == 0 && sh.xnan) sh.any_nan = 1;
+        __syncthreads();
+    }
     if (uniform_int(sh.any_nan)) {
         // NaN centroids (yakmo 0/0 means) make ANN's early exits order dependent:
         // this pass runs in the generic kernel (gsc_kernels.hip)
-        if (tid == 0) frp->generic = 1;
-        return;
+        if (tid == 0 && wg0) {
+            frp->generic = 1;
+            frp->xseq = (int)xp.seq;
+        }
+        break;
     }
 
     // wave-0 state: update log (lane = entry, tag = commit iteration) + residual (lane 0)
     int lg_pos = -1, lg_tag = 0;
     double err = 0.0;
     int slow_total = 0, restarts = 0;
+    bool guard = false;  // the progress guard tripped (identical in both workgroups)
 #ifdef GSC_STAMPS
     uint64_t acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tlast = stamp();
@@ -1044,50 +1194,60 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
         const bool has_p = nvq > 0;
         const int P_buf = vq_buf[0], P_s = vq_s[0], P_off = vq_off[0], P_n = has_p ? vq_n[0] : 0;
         // prefetch the next batch's queries (they land in LDS in part 3)
-        constexpr int PE = (kBatch * D + 64 * NW - 1) / (64 * NW);
+        constexpr int PE = (KB * D + nthreads - 1) / nthreads;
         float pre[PE];
 #pragma unroll
         for (int e = 0; e < PE; ++e) {
             const int k = tid + e * nthreads;
-            pre[e] = (k < kBatch * D && next_load + k / D < N) ? X[(int64_t)next_load * D + k] : 0.0f;
+            pre[e] = (k < KB * D && next_load + k / D < N) ? X[(int64_t)next_load * D + k] : 0.0f;
         }
         // ---- part 1: chain the pending batch's updates (wave 0); A1(current)
         VPState vst;
-        if (wave == 0 && has_p) vp_begin<D, LOGK>(sh, P_buf, P_off, P_n, vq_a1[0], lane, lg_pos, lg_tag, vst);
+        if (wave == 0 && has_p) vp_begin<C>(sh, P_buf, P_off, P_n, vq_a1[0], lane, lg_pos, lg_tag, vst);
         STAMP(0)
         // two queries per trip: one query's min-tree (a dependent DPP chain)
         // overlaps the other's distance FMAs
 #pragma unroll 1
         for (int jj = 0; jj < cur_n; jj += 2) {
             const int j1 = jj + 1 < cur_n ? jj + 1 : jj;
-            float dv0[8], dv1[8];
-            a1_dist_x2<D>(creg, cn, sh.qm[cur_buf][jj], sh.qm[cur_buf][j1], dv0, dv1);
-            a1_reduce2<LOGK>(dv0, dv1, sh.wrec[wave][jj], sh.wrec[wave][j1], wave, lane);
+            float dv0[SL], dv1[SL];
+            a1_dist_x2<D, SL>(creg, cn, sh.qm[cur_buf][jj], sh.qm[cur_buf][j1], dv0, dv1);
+            a1_reduce2<C>(dv0, dv1, sh.wrec[vwave][jj], sh.wrec[vwave][j1], vwave, lane);
             if (wave == 0 && has_p) {
-                vp_step(jj, lane, lg_pos, vst);
-                if (jj + 1 < cur_n) vp_step(jj + 1, lane, lg_pos, vst);
+                vp_step<C>(jj, lane, lg_pos, vst);
+                if (jj + 1 < cur_n) vp_step<C>(jj + 1, lane, lg_pos, vst);
             }
         }
         if (wave == 0 && has_p) {
 #pragma unroll 1
-            for (int k = cur_n; k < kBatch; ++k) vp_step(k, lane, lg_pos, vst);
-            vp_end<D, LOGK>(sh, P_buf, P_off, P_n, lane, lg_pos, vst);
+            for (int k = cur_n; k < KB; ++k) vp_step<C>(k, lane, lg_pos, vst);
+            vp_end<C>(sh, P_buf, P_off, P_n, lane, lg_pos, vst);
         }
         STAMP(1)
         lds_barrier();
         STAMP(6)
+        if constexpr (NWG == 2) {
+            if (cur_n > 0) {
+                write_cstar<C>(sh, creg, sh.qrec[cur_buf], (1ull << cur_n) - 1ull, 0, wave, lane, wg);
+                lds_barrier();
+                xchg_records<C>(sh, xp, cur_n, nullptr, 0, sh.qrec[cur_buf], tid, wg);
+                lds_barrier();
+                fill_winner_coords<C>(sh, sh.qrec[cur_buf], cur_n, nullptr, 0, tid, wg);
+            }
+        }
         // ---- part 2: check the pending batch; certificates of the current batch
-        if (has_p) v_check_q<D, LOGK, NW>(sh, P_buf, P_off, P_n, wave, lane);
+        if (has_p) v_check_q<C>(sh, P_buf, P_off, P_n, wave, lane);
         STAMP(7)
         if (cur_n > 0) {
             // c*'s snapshot coordinates (and exact distance), written by the wave that owns c*
-            write_cstar<D, NW>(sh, creg, cur_buf, (1ull << cur_n) - 1ull, wave, lane);
+            if constexpr (NWG == 1)
+                write_cstar<C>(sh, creg, sh.qrec[cur_buf], (1ull << cur_n) - 1ull, 0, wave, lane, 0);
             STAMP(8)
 #pragma unroll 1
-            for (int j0 = wave * 4; j0 < cur_n; j0 += 4 * NW)
-                a2_group<D, LOGK, NW, true>(sh, j0, cur_n, sh.q[cur_buf], sh.qrec[cur_buf], 0, nullptr, lane
+            for (int j0 = wave * 4; j0 < cur_n; j0 += 4 * NWL)
+                a2_group<C, true>(sh, j0, cur_n, sh.q[cur_buf], sh.qrec[cur_buf], 0, nullptr, lane
 #ifdef GSC_STAMPS
-                                      , acc, &tlast
+                                  , acc, &tlast
 #endif
                 );
         }
@@ -1104,13 +1264,21 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
                 while (m) {
                     const int jj = __ffsll((long long)m) - 1;
                     m &= m - 1;
-                    a1_query<D, LOGK>(creg, sh.q[cur_buf][jj], sh.wrec[wave][jj], wave, lane);
+                    a1_query<C>(creg, sh.q[cur_buf][jj], sh.wrec[vwave][jj], vwave, lane);
                 }
                 lds_barrier();
-                write_cstar<D, NW>(sh, creg, cur_buf, fx, wave, lane);
+                if constexpr (NWG == 2) {
+                    write_cstar<C>(sh, creg, sh.qrec[cur_buf], fx, 0, wave, lane, wg);
+                    lds_barrier();
+                    xchg_records<C>(sh, xp, nfx, sh.fxl, 0, sh.qrec[cur_buf], tid, wg);
+                    lds_barrier();
+                    fill_winner_coords<C>(sh, sh.qrec[cur_buf], nfx, sh.fxl, 0, tid, wg);
+                } else {
+                    write_cstar<C>(sh, creg, sh.qrec[cur_buf], fx, 0, wave, lane, 0);
+                }
 #pragma unroll 1
-                for (int j0 = wave * 4; j0 < nfx; j0 += 4 * NW)
-                    a2_group<D, LOGK, NW, false>(sh, j0, nfx, sh.q[cur_buf], sh.qrec[cur_buf], 0, sh.fxl, lane);
+                for (int j0 = wave * 4; j0 < nfx; j0 += 4 * NWL)
+                    a2_group<C, false>(sh, j0, nfx, sh.q[cur_buf], sh.qrec[cur_buf], 0, sh.fxl, lane);
                 lds_barrier();
             }
         }
@@ -1127,14 +1295,14 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
             const int k = fj >= 0 ? fj : P_n;
             const int j = lane;
             const bool cj = j < k;
-            const QRec& R = sh.qrec[P_buf][P_off + (cj ? j : 0)];
-            if (cj) {
+            const QRecT<D>& R = sh.qrec[P_buf][P_off + (cj ? j : 0)];
+            if (cj && wg0) {
                 clusters[P_s + P_off + j] = R.id;
                 atomicAdd(&cnta[R.cstar], 1);
             }
             const float sq = cj ? __fsqrt_rn(sh.gp[j] / (float)D) : 0.0f;
 #pragma unroll
-            for (int jj = 0; jj < kBatch; ++jj) {
+            for (int jj = 0; jj < KB; ++jj) {
                 const double t = (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(sq), jj));
                 err = jj < k ? err + t : err;
             }
@@ -1143,7 +1311,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
             const int k = fj >= 0 ? fj : P_n;
             const int j = lane;
             const bool cj = j < k;
-            const QRec& R = sh.qrec[P_buf][P_off + (cj ? j : 0)];
+            const QRecT<D>& R = sh.qrec[P_buf][P_off + (cj ? j : 0)];
             // the last committed update of each centroid becomes its log entry:
             // the entry already holding that centroid, else the r-th free entry
             const bool lastc = cj && sh.nxt[j] >= k;
@@ -1158,7 +1326,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
             if (lastc) {
 #pragma unroll
                 for (int d = 0; d < D; ++d) sh.lg_c[tgt][d] = sh.newc[j][d];
-                sh.lg_c[tgt][kRow - 1] = norm2_x<D>(sh.newc[j]);
+                sh.lg_c[tgt][C::ROW - 1] = norm2_x<D>(sh.newc[j]);
                 sh.asg[tgt] = R.cstar;
             }
             wave_lds_sync();
@@ -1199,7 +1367,7 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
         if (freeb >= 0 && !(fj >= 0 && freeb == P_buf) && next_load < N) {
             cur_buf = freeb;
             cur_s = next_load;
-            cur_n = min(kBatch, N - next_load);
+            cur_n = min(KB, N - next_load);
             next_load += cur_n;
 #pragma unroll
             for (int e = 0; e < PE; ++e) {
@@ -1217,72 +1385,102 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
         lds_barrier();
         STAMP(4)
         // ---- part 4: fold the log into the registers
-        refresh<D>(sh, creg, cn, cnmax, wave, lane);
+        refresh<C>(sh, creg, cn, cnmax, vwave, lane);
         if (solo_j >= 0) {
             // the failed query on the live centroids: fresh distances and
             // certificate; exact DFS if the certificate still fails
             ++restarts;
-            a1_query<D, LOGK>(creg, sh.qslow, sh.wrec[wave][kBatch], wave, lane);
+            a1_query<C>(creg, sh.qslow, sh.wrec[vwave][KB], vwave, lane);
             lds_barrier();
+            if constexpr (NWG == 2) {
+                write_cstar<C>(sh, creg, &sh.qsolo, 1ull, KB, wave, lane, wg);
+                lds_barrier();
+                xchg_records<C>(sh, xp, 1, nullptr, KB, &sh.qsolo, tid, wg);
+                lds_barrier();
+            }
             if (wave == 0)
-                a2_group<D, LOGK, NW, false>(sh, 0, 1, reinterpret_cast<const float(*)[16]>(sh.qslow), &sh.qsolo, kBatch,
-                                             nullptr, lane);
+                a2_group<C, false>(sh, 0, 1, reinterpret_cast<const float(*)[C::QD]>(sh.qslow), &sh.qsolo, KB,
+                                   nullptr, lane);
             lds_barrier();
             int bpos;
             float key;
+            bool dfs = false;
             STAMP(10)
             if (uniform_int(sh.qsolo.valid)) {
                 bpos = uniform_int(sh.qsolo.cstar);
                 key = sh.qsolo.g;
             } else {
-                float dv[8];
+                dfs = true;
+                float dv[SL];
 #pragma unroll
-                for (int s = 0; s < 8; ++s) dv[s] = 0.0f;
+                for (int s = 0; s < SL; ++s) dv[s] = 0.0f;
 #pragma unroll
                 for (int d = 0; d < D; ++d) {
                     const float qd = sh.qslow[d];
 #pragma unroll
-                    for (int s = 0; s < 8; ++s) {
+                    for (int s = 0; s < SL; ++s) {
                         const float t = fsub(qd, creg[s][d]);
                         dv[s] = fadd(dv[s], fmul(t, t));
                     }
                 }
 #pragma unroll
-                for (int s = 0; s < 8; ++s)
+                for (int s = 0; s < SL; ++s)
                     if (p0 + s < K) sh.dist[p0 + s] = dv[s];
+                if constexpr (NWG == 2) {  // the partner's half of the live distances
+                    lds_barrier();
+                    ++xp.seq;
+                    for (int i = tid; i < C::KG; i += nthreads) xput(xp, i, __float_as_uint(sh.dist[wg * C::KG + i]));
+                    for (int i = tid; i < C::KG; i += nthreads)
+                        sh.dist[(1 - wg) * C::KG + i] = __uint_as_float(xget(xp, i));
+                }
                 // the centroid registers wait in C (pass-start copy, rewritten at pass end)
                 // so the DFS has the register file
 #pragma unroll
-                for (int s = 0; s < 8; ++s)
+                for (int s = 0; s < SL; ++s)
                     if (p0 + s < K) {
                         const int id = sh.t.pidx[p0 + s];
 #pragma unroll
-                        for (int d = 0; d < D; ++d) C[(int64_t)id * D + d] = creg[s][d];
+                        for (int d = 0; d < D; ++d) C_[(int64_t)id * D + d] = creg[s][d];
                     }
                 __asm__ volatile("" ::: "memory");  // the reload below must not be forwarded from the stores
                 lds_barrier();  // sh.dist complete
-                dfs_parallel<D, LOGK, NW>(sh, tid, lane, wave, bpos, key);
+                dfs_parallel<C>(sh, tid, lane, wave, bpos, key);
                 bpos = uniform_int(bpos);
                 __asm__ volatile("" ::: "memory");
 #pragma unroll
-                for (int s = 0; s < 8; ++s)
+                for (int s = 0; s < SL; ++s)
                     if (p0 + s < K) {
                         const int id = sh.t.pidx[p0 + s];
 #pragma unroll
-                        for (int d = 0; d < D; ++d) creg[s][d] = C[(int64_t)id * D + d];
+                        for (int d = 0; d < D; ++d) creg[s][d] = C_[(int64_t)id * D + d];
                     }
                 ++slow_total;
                 STAMP(11)
             }
             // owner publishes c's coordinates; tid 0 moves it (encoder.lpr:735-744);
             // the move enters the log (later batches' snapshots miss it) and the registers
-            const int owner = bpos >> 3, slot = bpos & 7;
+            const int owner = bpos >> LS, slot = bpos & (SL - 1);
+            const int owner_t = owner - wg * C::NT;  // owner thread within this workgroup
 #pragma unroll
-            for (int s = 0; s < 8; ++s)
-                if (s == slot && tid == owner) {
+            for (int s = 0; s < SL; ++s)
+                if (s == slot && tid == owner_t) {
 #pragma unroll
                     for (int d = 0; d < D; ++d) sh.solo_c[d] = creg[s][d];
                 }
+            if constexpr (NWG == 2) {
+                lds_barrier();
+                const int owg = bpos / C::KG;
+                if (dfs) {  // the owner's coordinates of c (any leaf)
+                    ++xp.seq;
+                    if (tid < D) xput(xp, tid, __float_as_uint(sh.solo_c[tid]));
+                    if (tid < D) {
+                        const float v = __uint_as_float(xget(xp, tid));
+                        if (owg != wg) sh.solo_c[tid] = v;
+                    }
+                } else if (owg != wg && tid < D) {  // the certified winner: received with the records
+                    sh.solo_c[tid] = sh.lw_p[KB][tid];
+                }
+            }
             lds_barrier();
             if (wave == kErrWave && lane == 0) err += (double)__fsqrt_rn(key / (float)D);
             if (wave == 0) {
@@ -1292,8 +1490,10 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
                         const float o = sh.solo_c[d];
                         sh.solo_c[d] = fadd(o, fmul(fsub(sh.qslow[d], o), rate));
                     }
-                    atomicAdd(&cnta[bpos], 1);
-                    clusters[solo_j] = sh.t.pidx[bpos];
+                    if (wg0) {
+                        atomicAdd(&cnta[bpos], 1);
+                        clusters[solo_j] = sh.t.pidx[bpos];
+                    }
                 }
                 wave_lds_sync();
                 const uint64_t hit = __ballot(lg_pos == bpos);
@@ -1303,20 +1503,21 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
                     lg_tag = it;
 #pragma unroll
                     for (int d = 0; d < D; ++d) sh.lg_c[e][d] = sh.solo_c[d];
-                    sh.lg_c[e][kRow - 1] = norm2_x<D>(sh.solo_c);
+                    sh.lg_c[e][C::ROW - 1] = norm2_x<D>(sh.solo_c);
                 }
                 sh.pub_pos[lane] = lane == e ? bpos : -1;
             }
             lds_barrier();
-            refresh<D>(sh, creg, cn, cnmax, wave, lane);
+            refresh<C>(sh, creg, cn, cnmax, vwave, lane);
         }
         STAMP(5)
         if (nvq == 0 && cur_n == 0) {
-            if (tid == 0) frp->loop_iters = it + 1;
+            if (tid == 0 && wg0) frp->loop_iters = it + 1;
             break;
         }
         if (it > 4 * N + 64) {  // progress guard: every iteration commits or computes
-            if (tid == 0) frp->loop_iters = -1;
+            if (tid == 0 && wg0) frp->loop_iters = -1;
+            guard = true;
             break;
         }
     }
@@ -1325,35 +1526,42 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
     err = sh.err_out;
     // write back the live centroids and this pass's counts (cnts[Odd(iter)])
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
+    for (int s = 0; s < SL; ++s) {
         const int p = p0 + s;
         if (p < K) {
             const int id = sh.t.pidx[p];
 #pragma unroll
-            for (int d = 0; d < D; ++d) C[(int64_t)id * D + d] = creg[s][d];
-            // the commits' atomics live in L2: read past this CU's L1
-            prev_cnt[id] = __hip_atomic_load(&cnta[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int d = 0; d < D; ++d) C_[(int64_t)id * D + d] = creg[s][d];
         }
     }
+    if (wg0)
+        for (int p = tid; p < K; p += nthreads)  // the commits' atomics live in L2: read past this CU's L1
+            prev_cnt[sh.t.pidx[p]] = __hip_atomic_load(&cnta[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef GSC_STAMPS
-    if (lane == 0)
+    if (lane == 0 && wg0)
         for (int k = 0; k < 16; ++k) frp->stamps[wave * 16 + k] += acc[k];
 #endif
-    if (tid == 0) {
-        const double prev_err = pass == 0 ? 3.4028234663852886e+38 : frp->err;  // err := MaxSingle
-        const double diff = err > prev_err ? err - prev_err : prev_err - err;
+    const double diff = err > prev_err ? err - prev_err : prev_err - err;
+    const bool done = diff <= tol || pass + 1 >= kMaxScanIters || guard;
+    prev_err = err;
+    if (tid == 0 && wg0) {
         frp->iters = pass + 1;
         frp->slow += slow_total;
         frp->restarts += restarts;
         frp->err = err;
-        frp->done = (diff <= tol || pass + 1 >= kMaxScanIters || frp->loop_iters < 0) ? 1 : 0;
-        sh.pass_done = frp->done;
+        frp->done = done ? 1 : 0;
     }
     // the next pass's tree build and rate lookups read C and prev_cnt as
-    // written above by other lanes: agent fence (L1 invalidate) + barrier
-    __threadfence();
-    __syncthreads();
-    if (uniform_int(sh.pass_done)) break;
+    // written above by other lanes (and, two-CU frames, by the partner)
+    if constexpr (NWG == 2) {
+        pair_barrier(xp, tid);
+        if (tid == 0 && wg0) frp->xseq = (int)xp.seq;
+    } else {
+        __threadfence();
+        __syncthreads();
+    }
+    if (done) break;
+    }
     }
 }
 
@@ -1361,28 +1569,49 @@ __global__ __launch_bounds__(512) void scan_batch_kernel(ReduceFrame* __restrict
 
 using namespace gsc;
 
-// Batched KNNScanReduce for every frame (K = 2^logk, 256..4096, D = 8 or 16):
-// each frame runs its passes from frp->iters until it converges, reaches
-// max_passes or meets a NaN pass (left to the generic kernel).  Returns
-// hipErrorInvalidValue for shapes it does not cover.
-extern "C" hipError_t gsc_launch_scan_batch(int D, int logk, ReduceFrame* frames, int nframes, const float* X,
-                                            float* C, int* is, const float* rate_tab, double tol, int max_passes,
-                                            hipStream_t st) {
-    const int K = 1 << logk;
-    const int threads = 64 * (K >= 512 ? K / 512 : 1);
-    const size_t shm = sizeof(Scan2Shared);
-#define SB(DV, LK)                                                                                                     \
-    if (D == DV && logk == LK) {                                                                                       \
-        (void)hipFuncSetAttribute((const void*)scan_batch_kernel<DV, LK>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                  (int)shm);                                                                           \
-        hipLaunchKernelGGL((scan_batch_kernel<DV, LK>), dim3(nframes), dim3(threads), shm, st, frames, nframes, X, C,   \
-                           is, rate_tab, tol, max_passes);                                                                   \
-        return hipGetLastError();                                                                                      \
+template <class C>
+static hipError_t launch_scan(ReduceFrame* frames, int nframes, const float* X, float* Cc, int* is,
+                              const float* rate_tab, double tol, int max_passes, uint64_t* xbuf, hipStream_t st) {
+    const size_t shm = sizeof(Scan2Shared<C>);
+    static_assert(sizeof(Scan2Shared<C>) <= 160 * 1024, "LDS budget (160 KB per CU)");
+    hipError_t e = hipFuncSetAttribute((const void*)scan_batch_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)shm);
+    if (e != hipSuccess) return e;
+    if constexpr (C::NWG == 1) {
+        hipLaunchKernelGGL(scan_batch_kernel<C>, dim3(nframes), dim3(C::NT), shm, st, frames, nframes, X, Cc, is,
+                           rate_tab, tol, max_passes, xbuf);
+        return hipGetLastError();
+    } else {
+        // both workgroups of a frame must be resident together: a cooperative
+        // grid of at most one workgroup per CU, frame pairs looping over frames
+        int dev = 0, cus = 0;
+        if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+        if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+        int pairs = std::min(nframes, std::max(1, cus / 2));
+        if (pairs >= 8) pairs -= pairs % 8;  // whole groups of 16 workgroups: pair members share an XCD
+        void* args[] = {&frames, &nframes, &X, &Cc, &is, &rate_tab, &tol, &max_passes, &xbuf};
+        return hipLaunchCooperativeKernel((const void*)scan_batch_kernel<C>, dim3(2 * pairs), dim3(C::NT), args, shm,
+                                          st);
     }
-    SB(8, 8) SB(8, 9) SB(8, 10) SB(8, 11) SB(8, 12)
-    SB(16, 8) SB(16, 9) SB(16, 10) SB(16, 11) SB(16, 12)
+}
+
+// Batched KNNScanReduce for every frame (K = 2^logk, 256..4096; D = 8 or 16,
+// and D = 32 with two CUs per frame at K = 4096): each frame runs its passes
+// from frp->iters until it converges, reaches max_passes or meets a NaN pass
+// (left to the generic kernel).  xbuf: 2 x 2 x 2048 zeroed granules per frame
+// (D = 32, K = 4096 only).  Returns hipErrorInvalidValue for shapes it does
+// not cover.
+extern "C" hipError_t gsc_launch_scan_batch(int D, int logk, ReduceFrame* frames, int nframes, const float* X,
+                                            float* Cc, int* is, const float* rate_tab, double tol, int max_passes,
+                                            uint64_t* xbuf, hipStream_t st) {
+#define SB(DV, LK, SLV, NG)                                                                                    \
+    if (D == DV && logk == LK)                                                                                 \
+        return launch_scan<ScanCfg<DV, LK, SLV, NG>>(frames, nframes, X, Cc, is, rate_tab, tol, max_passes, xbuf, st);
+    SB(8, 8, 8, 1) SB(8, 9, 8, 1) SB(8, 10, 8, 1) SB(8, 11, 8, 1) SB(8, 12, 8, 1)
+    SB(16, 8, 8, 1) SB(16, 9, 8, 1) SB(16, 10, 8, 1) SB(16, 11, 8, 1) SB(16, 12, 8, 1)
+    SB(32, 8, 4, 1) SB(32, 9, 4, 1) SB(32, 10, 4, 1) SB(32, 11, 4, 1) SB(32, 12, 4, 2)
 #undef SB
     return hipErrorInvalidValue;
 }
 
-extern "C" size_t gsc_scan_batch_shared_bytes(void) { return sizeof(Scan2Shared); }
+extern "C" size_t gsc_scan_xbuf_granules_per_frame(void) { return 2 * 2 * (size_t)kXCap; }

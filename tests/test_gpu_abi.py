@@ -128,7 +128,8 @@ def test_knnfit_replay_matches_oracle(oracle, frame):
     q = np.ascontiguousarray(frame["knn_query"][:1500])
     eps = np.float32(frame["knn_eps"])
     CS = cand.shape[1]
-    kdt = lib.ann_kdtree_create(_rows(cand), cand.shape[0], CS, 1, 0)
+    pa = _rows(cand)  # the tree keeps the row-pointer array (ANN does not copy it): keep it alive
+    kdt = lib.ann_kdtree_create(pa, cand.shape[0], CS, 1, 0)
     assert kdt
     idxs = np.zeros(64, np.int32)
     errs = np.zeros(64, np.float32)

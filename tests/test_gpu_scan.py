@@ -60,7 +60,52 @@ def test_scan_k4096_full(c2_trace):
     np.testing.assert_array_equal(_bits(gc), _bits(c2_trace["scan"]))
 
 
-@pytest.mark.parametrize("name", ["hihat_cs8_cpf256", "silence_tone_cs8_cpf256"])
+@pytest.fixture(scope="module")
+def c3_trace(oracle):
+    make, argv = CASES["syn8s_c3_cs16_cpf4096_cbd12"]
+    return oracle.trace_frame(make(), argv, 0)
+
+
+@pytest.mark.parametrize("passes", [1, 3])
+def test_scan_k4096_d32_first_passes(oracle, c3_trace, passes):
+    """D = 32 (ChunkSize 16): each frame on two CUs exchanging A1 records."""
+    import soundchunks_amd as sc
+
+    os.environ["GSC_SCAN_MAX_PASSES"] = str(passes)
+    try:
+        gc, gcl, gn = sc.scan_reduce(c3_trace["dataset"], c3_trace["yakmo"], precision=3)
+    finally:
+        del os.environ["GSC_SCAN_MAX_PASSES"]
+    oc, ocl, on = oracle.scan_reduce(c3_trace["dataset"], c3_trace["yakmo"], 3, passes)
+    assert gn == on == passes
+    np.testing.assert_array_equal(gcl, ocl)
+    np.testing.assert_array_equal(_bits(gc), _bits(oc))
+
+
+def test_scan_k4096_d32_full(c3_trace):
+    import soundchunks_amd as sc
+
+    gc, gcl, gn = sc.scan_reduce(c3_trace["dataset"], c3_trace["yakmo"], precision=3)
+    assert gn == c3_trace["scan_iters"]
+    np.testing.assert_array_equal(gcl, c3_trace["clusters"])
+    np.testing.assert_array_equal(_bits(gc), _bits(c3_trace["scan"]))
+
+
+@pytest.mark.parametrize("k", [256, 2048])
+def test_scan_d32_one_cu(oracle, c3_trace, k):
+    """D = 32 with K <= 2048 fits one CU (4 leaves per lane)."""
+    import soundchunks_amd as sc
+
+    x = c3_trace["dataset"][:6000]
+    c0 = sc.yakmo_seed_means(x, k)
+    gc, gcl, gn = sc.scan_reduce(x, c0, precision=3)
+    oc, ocl, on = oracle.scan_reduce(x, c0, 3, 100)
+    assert gn == on
+    np.testing.assert_array_equal(gcl, ocl)
+    np.testing.assert_array_equal(_bits(gc), _bits(oc))
+
+
+@pytest.mark.parametrize("name", ["hihat_cs8_cpf256", "silence_tone_cs8_cpf256", "quiet_tone_cs8_cpf1024"])
 def test_generic_scan_kernel_still_exact(name):
     # the generic per-search kernel (non-power-of-2 K, NaN passes) on its own
     code = (f"import sys; sys.path[:0]=[{str(ROOT)!r},{str(ROOT / 'tests')!r}];"
