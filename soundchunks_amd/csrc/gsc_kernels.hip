@@ -272,6 +272,10 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
                 }
             }
             const uint64_t farmask = __ballot(far);
+            // a NaN box' (a NaN cut value or cell bound: NaN centroids) fails
+            // ANN's visit test (box' < max_key) whatever the distances, and
+            // fmaxf below would drop it from B: such paths take the exact DFS
+            const bool nanbox = __ballot(far && inc != inc) != 0;
             // box' = ((root + inc_a) + inc_b) + ... over far steps, in depth order
             float box = rootbox;
             float boxp = -__builtin_inff();
@@ -316,7 +320,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
                     }
                 }
             }
-            fast = __all(ok);
+            fast = __all(ok) && !nanbox;
         }
         if (lane == 0) sh.wok[wave] = fast ? 1 : 0;
         lds_barrier();

@@ -54,14 +54,24 @@
 // the unique minimum is never replaced.  A centroid u moved after the
 // snapshot keeps the proof iff its live distance d_u > d(c*) and, when its
 // LCA with c* is a far step, d_u > B[lca]; a moved c* needs d(c*) < m2.
+#include <type_traits>
+
 #include "gsc_tree.h"
 
 namespace gsc {
 
-// Shape of one KNNScanReduce pipeline instance.
-template <int D_, int LOGK_, int SL_, int NWG_>
+template <int SL>
+struct WaveRecT;
+struct MRec;
+
+// Shape of one KNNScanReduce pipeline instance.  MF: the matrix-core layout
+// (A1 bounds on v_mfma_f32_16x16x4_f32; see "MFMA layout" below).
+template <int D_, int LOGK_, int SL_, int NWG_, bool MF_ = false>
 struct ScanCfg {
     static constexpr int D = D_, LOGK = LOGK_, SL = SL_, NWG = NWG_;
+    static constexpr bool MF = MF_;
+    static constexpr int RT = MF ? 32 : SL;     // register tiles (MF) / leaf slots per lane
+    static constexpr int RD = MF ? D / 4 : D;   // floats per tile / slot per lane
     static constexpr int K = 1 << LOGK;
     static constexpr int LS = SL == 8 ? 3 : (SL == 4 ? 2 : 1);        // log2 slots per lane
     static constexpr int LPW = 64 * SL;                                 // leaves per wave
@@ -80,6 +90,8 @@ struct ScanCfg {
     static_assert(NWV <= 16, "A2 evaluates up to 16 wave records per query (one per lane of a 16-lane group)");
     static_assert(KB <= 32 && 64 % KB == 0, "batch size");
     static_assert(NWG == 1 || (FULL && NWL == 8), "two-CU frames: 8 full waves per workgroup");
+    static_assert(!MF || (SL == 8 && NWG == 1 && FULL && (D == 8 || D == 16)), "MFMA layout: 512 leaves per wave");
+    using Rec = std::conditional_t<MF, MRec, WaveRecT<SL>>;
 };
 
 // float minimum on f32 bit patterns (A1 values may be negative: the batch
@@ -627,6 +639,7 @@ __device__ __forceinline__ void a2_group(Scan2Shared<C>& sh, int j0, int nq, con
         unique = !tie;
         m2lo = __uint_as_float(m2);
     }
+    if (far && inc != inc) ok = false;  // a NaN box' is never visited (fmaxf would drop it from B)
     const bool gok = ((__ballot(!ok) >> gbase) & 0xFFFFull) == 0;
     const bool valid = unique && __uint_as_float(gmin) <= FLT_MAX && gok;
     if (qa) {
