@@ -162,7 +162,13 @@ struct QRecT {        // A2 output per query
 template <class C>
 struct Scan2Shared {
     KdTree t;
-    float dist[kMaxK];     // tree build scratch; live distances for the exact DFS
+    // tree build scratch and the exact DFS's live distances share the bytes of
+    // the A1 records: the records are dead at pass start and once the solo
+    // query's certificate has failed
+    union {
+        float dist[kMaxK];
+        WaveRecT<C::SL> wrec[C::NWV][C::KB + 1];  // column KB: the solo query
+    };
     float rate[kMaxK];     // Single(1/sqrt(cnts[not Odd(iter)])) by kd-leaf position
     float dfs_inc[kMaxK];  // exact DFS: per split node box' increment, sign = near child hi
     alignas(16) float q[2][C::KB][C::QD];
@@ -170,7 +176,6 @@ struct Scan2Shared {
     float cnmax[C::NWV];   // per (virtual) wave: upper bound of |c|^2 over its live centroids (monotone within a pass)
     int fxl[C::KB];        // queries of the current batch re-certified exactly
     alignas(16) float qslow[C::QD];  // the query resolved on its own after a failed commit
-    WaveRecT<C::SL> wrec[C::NWV][C::KB + 1];  // column KB: the solo query
     alignas(16) QRecT<C::D> qrec[2][C::KB];
     QRecT<C::D> qsolo;
     // update log: entry e = wave-0 lane e (position in a VGPR, coordinates here)
@@ -1199,13 +1204,15 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
 #endif
     // batches awaiting commit, in order: buffer, first query of the buffer,
     // first uncommitted slot, count, iteration of their distance snapshot
-    int vq_buf[2] = {0, 0}, vq_s[2] = {0, 0}, vq_off[2] = {0, 0}, vq_n[2] = {0, 0}, vq_a1[2] = {0, 0};
+    // (two named slots, not arrays: a runtime-indexed array would live in scratch)
+    int vq_buf0 = 0, vq_s0 = 0, vq_off0 = 0, vq_n0 = 0, vq_a10 = 0;
+    int vq_buf1 = 0, vq_s1 = 0, vq_off1 = 0, vq_n1 = 0, vq_a11 = 0;
     int nvq = 0;
     int cur_buf = 0, cur_s = 0, cur_n = n0;  // batch whose distances are computed this iteration
     int next_load = n0;
     for (int it = 0;; ++it) {
         const bool has_p = nvq > 0;
-        const int P_buf = vq_buf[0], P_s = vq_s[0], P_off = vq_off[0], P_n = has_p ? vq_n[0] : 0;
+        const int P_buf = vq_buf0, P_s = vq_s0, P_off = vq_off0, P_n = has_p ? vq_n0 : 0;
         // prefetch the next batch's queries (they land in LDS in part 3)
         constexpr int PE = (KB * D + nthreads - 1) / nthreads;
         float pre[PE];
@@ -1216,7 +1223,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         }
         // ---- part 1: chain the pending batch's updates (wave 0); A1(current)
         VPState vst;
-        if (wave == 0 && has_p) vp_begin<C>(sh, P_buf, P_off, P_n, vq_a1[0], lane, lg_pos, lg_tag, vst);
+        if (wave == 0 && has_p) vp_begin<C>(sh, P_buf, P_off, P_n, vq_a10, lane, lg_pos, lg_tag, vst);
         STAMP(0)
         // two queries per trip: one query's min-tree (a dependent DPP chain)
         // overlaps the other's distance FMAs
@@ -1354,29 +1361,37 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         const int solo_j = fj >= 0 ? P_s + P_off + fj : -1;
         if (has_p) {
             if (fj >= 0 && fj + 1 < P_n) {
-                vq_off[0] = P_off + fj + 1;
-                vq_n[0] = P_n - fj - 1;
+                vq_off0 = P_off + fj + 1;
+                vq_n0 = P_n - fj - 1;
             } else {
-                vq_buf[0] = vq_buf[1];
-                vq_s[0] = vq_s[1];
-                vq_off[0] = vq_off[1];
-                vq_n[0] = vq_n[1];
-                vq_a1[0] = vq_a1[1];
+                vq_buf0 = vq_buf1;
+                vq_s0 = vq_s1;
+                vq_off0 = vq_off1;
+                vq_n0 = vq_n1;
+                vq_a10 = vq_a11;
                 --nvq;
             }
         }
         if (cur_n > 0) {
-            vq_buf[nvq] = cur_buf;
-            vq_s[nvq] = cur_s;
-            vq_off[nvq] = 0;
-            vq_n[nvq] = cur_n;
-            vq_a1[nvq] = it;
+            if (nvq == 0) {
+                vq_buf0 = cur_buf;
+                vq_s0 = cur_s;
+                vq_off0 = 0;
+                vq_n0 = cur_n;
+                vq_a10 = it;
+            } else {
+                vq_buf1 = cur_buf;
+                vq_s1 = cur_s;
+                vq_off1 = 0;
+                vq_n1 = cur_n;
+                vq_a11 = it;
+            }
             ++nvq;
         }
         // next batch of distances: into a free buffer, never the buffer a
         // failed query's coordinates are being copied out of (wave 0, above)
         cur_n = 0;
-        const int freeb = nvq == 0 ? (fj >= 0 ? P_buf ^ 1 : 0) : (nvq == 1 ? vq_buf[0] ^ 1 : -1);
+        const int freeb = nvq == 0 ? (fj >= 0 ? P_buf ^ 1 : 0) : (nvq == 1 ? vq_buf0 ^ 1 : -1);
         if (freeb >= 0 && !(fj >= 0 && freeb == P_buf) && next_load < N) {
             cur_buf = freeb;
             cur_s = next_load;

@@ -1,0 +1,31 @@
+"""Phase stamps of the batched KNNScanReduce kernel on one C2 frame (GPU box).
+Build the stamps library first (make -C soundchunks_amd/csrc stamps), then:
+    GSC_LIB=soundchunks_amd/lib/stamps/libsoundchunks_amd.so GSC_SCAN_DEBUG=1 \
+        python tools/scan_stamps.py [passes] [cs]
+GSC_SCAN_LANE_LAYOUT=1 selects the VALU-only A1 layout."""
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+import numpy as np  # noqa: E402
+
+import soundchunks_amd as sc  # noqa: E402
+from soundchunks_amd.synth import synth_wav  # noqa: E402
+
+passes = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+cs = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+argv = [f"-cs{cs}", "-cpf4096", "-cbd8"]
+wav = synth_wav(8.0)
+att, feat = sc.frame_dsp(wav, 0, argv)
+y = sc.yakmo_seed_means(feat, 4096)
+os.environ["GSC_SCAN_MAX_PASSES"] = str(passes)
+t = time.time()
+c, cl, it = sc.scan_reduce(feat, y, 3)
+dt = time.time() - t
+print(f"layout={'lane' if os.environ.get('GSC_SCAN_LANE_LAYOUT') else 'mfma'} N={feat.shape[0]} D={feat.shape[1]} "
+      f"passes={it} wall={dt:.3f}s us/search={dt / (it * feat.shape[0]) * 1e6:.3f} "
+      f"crc={int(np.frombuffer(c.tobytes(), np.uint32).sum()) & 0xffffffff:08x}", flush=True)
