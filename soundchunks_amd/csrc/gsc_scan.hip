@@ -54,24 +54,14 @@
 // the unique minimum is never replaced.  A centroid u moved after the
 // snapshot keeps the proof iff its live distance d_u > d(c*) and, when its
 // LCA with c* is a far step, d_u > B[lca]; a moved c* needs d(c*) < m2.
-#include <type_traits>
-
 #include "gsc_tree.h"
 
 namespace gsc {
 
-template <int SL>
-struct WaveRecT;
-struct MRec;
-
-// Shape of one KNNScanReduce pipeline instance.  MF: the matrix-core layout
-// (A1 bounds on v_mfma_f32_16x16x4_f32; see "MFMA layout" below).
-template <int D_, int LOGK_, int SL_, int NWG_, bool MF_ = false>
+// Shape of one KNNScanReduce pipeline instance.
+template <int D_, int LOGK_, int SL_, int NWG_>
 struct ScanCfg {
     static constexpr int D = D_, LOGK = LOGK_, SL = SL_, NWG = NWG_;
-    static constexpr bool MF = MF_;
-    static constexpr int RT = MF ? 32 : SL;     // register tiles (MF) / leaf slots per lane
-    static constexpr int RD = MF ? D / 4 : D;   // floats per tile / slot per lane
     static constexpr int K = 1 << LOGK;
     static constexpr int LS = SL == 8 ? 3 : (SL == 4 ? 2 : 1);        // log2 slots per lane
     static constexpr int LPW = 64 * SL;                                 // leaves per wave
@@ -90,8 +80,6 @@ struct ScanCfg {
     static_assert(NWV <= 16, "A2 evaluates up to 16 wave records per query (one per lane of a 16-lane group)");
     static_assert(KB <= 32 && 64 % KB == 0, "batch size");
     static_assert(NWG == 1 || (FULL && NWL == 8), "two-CU frames: 8 full waves per workgroup");
-    static_assert(!MF || (SL == 8 && NWG == 1 && FULL && (D == 8 || D == 16)), "MFMA layout: 512 leaves per wave");
-    using Rec = std::conditional_t<MF, MRec, WaveRecT<SL>>;
 };
 
 // float minimum on f32 bit patterns (A1 values may be negative: the batch
@@ -174,6 +162,11 @@ struct Scan2Shared {
     alignas(16) float q[2][C::KB][C::QD];
     alignas(16) float qm[2][C::KB][C::QD];  // -2 q (exact), the A1 dot-product operand
     float cnmax[C::NWV];   // per (virtual) wave: upper bound of |c|^2 over its live centroids (monotone within a pass)
+    // A1 pruning (one-CU frames): per wave the bounding box of its centroids'
+    // live register coordinates (grown by every fold), per batch query an
+    // upper bound of the snapshot's minimum distance
+    float wlo[C::NWV][C::D], whi[C::NWV][C::D];
+    uint32_t ub[C::KB];
     int fxl[C::KB];        // queries of the current batch re-certified exactly
     alignas(16) float qslow[C::QD];  // the query resolved on its own after a failed commit
     alignas(16) QRecT<C::D> qrec[2][C::KB];
@@ -333,6 +326,80 @@ __device__ __forceinline__ void pair_barrier(XPort& x, int tid) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// A1 pruning.  ANN's DFS reaches ~170 of the 4096 leaves per search on the
+// benchmark data; the batched A1 evaluates all of them.  A wave can skip a
+// query when no leaf of its 512 can be the answer: lb = box distance from q
+// to the bounding box of the wave's centroids (their live register values,
+// the box grown at every fold) is a lower bound of every leaf distance there,
+// so lb > ub + 4 eps, with ub >= the snapshot's minimum distance, proves the
+// wave holds neither c* nor a leaf within the certificate's margins.  ub comes
+// from the query's home waves (those whose box contains q: lb = 0), which
+// evaluate first; the others decide after one barrier.  (Homes by kd descent
+// instead of boxes cover the ~20 % of queries outside every box, but cost the
+// kernel 30 more spilled VGPRs and were slower: 5464 vs 5285 ms.)  A skipped wave's
+// record carries a valid lower bound of its A1 values instead of a minimum:
+//   approximate records (s~ = d~ - |q|^2):  v = (lb - 3 eps) - |q|^2,
+//   exact records (fixups):                 v = lb,
+// so every certificate inequality A2 evaluates with it stays sound (the
+// bound only stands in for minima of other waves and never wins).
+// Rounding: lb is a sequential f32 sum (relative error < (D+2) u), scaled by
+// (1 - 2^-17) below the real box distance, which is <= every exact f32
+// distance scaled by 1 + (D+1) u; eps >= 2^-5 x the roundings of the bound
+// arithmetic (|lb|, |q|^2, |d~| <= 2 (|q|^2 + M)).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int wave_min_i(int v) {
+    v = min(v, (int)partner<0>((uint32_t)v));
+    v = min(v, (int)partner<1>((uint32_t)v));
+    v = min(v, (int)partner<2>((uint32_t)v));
+    v = min(v, (int)partner<3>((uint32_t)v));
+    v = min(v, (int)partner<4>((uint32_t)v));
+    return min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 32));
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+    v = max(v, (int)partner<0>((uint32_t)v));
+    v = max(v, (int)partner<1>((uint32_t)v));
+    v = max(v, (int)partner<2>((uint32_t)v));
+    v = max(v, (int)partner<3>((uint32_t)v));
+    v = max(v, (int)partner<4>((uint32_t)v));
+    return max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 32));
+}
+
+// pass start: the box of this wave's leaves
+template <class C>
+__device__ __forceinline__ void wave_box_init(Scan2Shared<C>& sh, const float (&creg)[C::SL][C::D], int vwave, int lane,
+                                              int p0) {
+#pragma unroll  // static register indices: a runtime d would demote creg to scratch
+    for (int d = 0; d < C::D; ++d) {
+        float lo = __builtin_inff(), hi = -__builtin_inff();
+#pragma unroll
+        for (int s = 0; s < C::SL; ++s)
+            if (p0 + s < C::K) {
+                lo = fminf(lo, creg[s][d]);
+                hi = fmaxf(hi, creg[s][d]);
+            }
+        const int klo = wave_min_i(ordkey(__float_as_uint(lo)));
+        const int khi = wave_max_i(ordkey(__float_as_uint(hi)));
+        if (lane == 0) {
+            sh.wlo[vwave][d] = __uint_as_float(keybits(klo));
+            sh.whi[vwave][d] = __uint_as_float(keybits(khi));
+        }
+    }
+}
+
+// lower bound of every exact leaf distance in wave w's box (0 inside the box)
+template <class C>
+__device__ __forceinline__ float wave_box_lb(const Scan2Shared<C>& sh, const float* __restrict__ q, int w) {
+    float lb = 0.0f;
+#pragma unroll
+    for (int d = 0; d < C::D; ++d) {
+        const float qd = q[d], lo = sh.wlo[w][d], hi = sh.whi[w][d];
+        const float t = lo > qd ? fsub(lo, qd) : (qd > hi ? fsub(qd, hi) : 0.0f);
+        lb = fadd(lb, fmul(t, t));
+    }
+    return fmul(lb, 1.0f - 0x1p-17f);
 }
 
 // ---------------------------------------------------------------------------
@@ -916,6 +983,11 @@ __device__ __forceinline__ void refresh(Scan2Shared<C>& sh, float (&creg)[C::SL]
         const float nv = sh.lg_c[e][C::ROW - 1];  // |c|^2, written with the entry
         // the wave's norm bound only grows within a pass (A2 reads it for any earlier snapshot)
         cnmax = fmaxf(cnmax, nv);
+        if (C::NWG == 1 && lane < D) {  // the pruning box covers the new position
+            const float v = sh.lg_c[e][lane];
+            sh.wlo[vwave][lane] = fminf(sh.wlo[vwave][lane], v);
+            sh.whi[vwave][lane] = fmaxf(sh.whi[vwave][lane], v);
+        }
 #pragma unroll
         for (int s = 0; s < SL; ++s) {
             if (s == slot) {
@@ -1076,6 +1148,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                                                            int max_passes, uint64_t* __restrict__ xbuf) {
     constexpr int D = C::D, K = C::K, SL = C::SL, LS = C::LS, NWL = C::NWL, KB = C::KB, NWG = C::NWG;
     constexpr int kErrWave = NWL > 1 ? 1 : 0;  // residual + cluster ids (wave 0 keeps the log)
+    constexpr bool PRUNE = NWG == 1;           // A1 pruning by wave boxes (one-CU frames)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Scan2Shared<C>& sh = *reinterpret_cast<Scan2Shared<C>*>(smem);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1164,6 +1237,10 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         cnmax = wave_max_nonneg(nan_here ? 0.0f : mx);  // NaN passes leave for the generic kernel below
         if (lane == 0) sh.cnmax[vwave] = cnmax;
     }
+    if constexpr (PRUNE) {
+        wave_box_init<C>(sh, creg, vwave, lane, p0);
+        if (tid < KB) sh.ub[tid] = kInfBits;
+    }
     // first batch's queries
     const int n0 = min(KB, N);
     for (int k = tid; k < n0 * D; k += nthreads) {
@@ -1225,22 +1302,62 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         VPState vst;
         if (wave == 0 && has_p) vp_begin<C>(sh, P_buf, P_off, P_n, vq_a10, lane, lg_pos, lg_tag, vst);
         STAMP(0)
-        // two queries per trip: one query's min-tree (a dependent DPP chain)
-        // overlaps the other's distance FMAs
+        int kstep = 0;  // wave 0: chain steps taken
+        // A1 of the queries in mask m, two per trip: one query's min-tree (a
+        // dependent DPP chain) overlaps the other's distance FMAs
+        auto a1_mask = [&](uint64_t m) {
 #pragma unroll 1
-        for (int jj = 0; jj < cur_n; jj += 2) {
-            const int j1 = jj + 1 < cur_n ? jj + 1 : jj;
-            float dv0[SL], dv1[SL];
-            a1_dist_x2<D, SL>(creg, cn, sh.qm[cur_buf][jj], sh.qm[cur_buf][j1], dv0, dv1);
-            a1_reduce2<C>(dv0, dv1, sh.wrec[vwave][jj], sh.wrec[vwave][j1], vwave, lane);
-            if (wave == 0 && has_p) {
-                vp_step<C>(jj, lane, lg_pos, vst);
-                if (jj + 1 < cur_n) vp_step<C>(jj + 1, lane, lg_pos, vst);
+            while (m) {
+                const int j0 = __ffsll((long long)m) - 1;
+                m &= m - 1;
+                const int j1 = m ? __ffsll((long long)m) - 1 : j0;
+                if (m) m &= m - 1;
+                float dv0[SL], dv1[SL];
+                a1_dist_x2<D, SL>(creg, cn, sh.qm[cur_buf][j0], sh.qm[cur_buf][j1], dv0, dv1);
+                a1_reduce2<C>(dv0, dv1, sh.wrec[vwave][j0], sh.wrec[vwave][j1], vwave, lane);
+                if (wave == 0 && has_p) {
+                    if (kstep < KB) vp_step<C>(kstep++, lane, lg_pos, vst);
+                    if (kstep < KB) vp_step<C>(kstep++, lane, lg_pos, vst);
+                }
             }
+        };
+        const uint64_t curm = cur_n > 0 ? (cur_n >= 64 ? ~0ull : (1ull << cur_n) - 1ull) : 0ull;
+        uint64_t prunedm = 0;  // queries this wave skipped (wave-uniform)
+        float lbp = 0.0f, qn_j = 0.0f, eps_j = 0.0f;  // lane j: query j's box bound, |q|^2, eps
+        if constexpr (PRUNE) {
+            if (cur_n > 0) {
+                const int jr = lane < cur_n ? lane : 0;
+                const float* qv = sh.q[cur_buf][jr];
+                lbp = wave_box_lb<C>(sh, qv, vwave);
+                qn_j = norm2_x<D>(qv);
+                float M = 0.0f;
+#pragma unroll
+                for (int w = 0; w < C::NWV; ++w) M = fmaxf(M, sh.cnmax[w]);
+                eps_j = fadd(fmul(fadd(qn_j, M), C::EPSF), 1e-37f);
+                // home queries (q inside this wave's box) first: their minima bound
+                // the others (a query outside every box is evaluated by all waves)
+                const uint64_t home = __ballot(lbp == 0.0f) & curm;
+                a1_mask(home);
+                wave_lds_sync();
+                if ((home >> lane) & 1ull) {
+                    const float m = __uint_as_float(sh.wrec[vwave][lane].minbits);
+                    const float ubd = fmul(fadd(fadd(qn_j, m), eps_j), 1.0f + 0x1p-20f);
+                    atomicMin(&sh.ub[lane], __float_as_uint(fmaxf(ubd, 0.0f)));
+                }
+                lds_barrier();
+                const float ubj = __uint_as_float(sh.ub[jr]);
+                const float thr = fmul(fadd(ubj, fmul(4.0f, eps_j)), 1.0f + 0x1p-20f);
+                prunedm = __ballot(lbp > thr) & curm & ~home;
+                if ((prunedm >> lane) & 1ull)  // a lower bound of this wave's A1 values (see above)
+                    sh.wrec[vwave][lane].minbits = __float_as_uint(fsub(fsub(lbp, fmul(3.0f, eps_j)), qn_j));
+                a1_mask(curm & ~home & ~prunedm);
+            }
+        } else {
+            a1_mask(curm);
         }
         if (wave == 0 && has_p) {
 #pragma unroll 1
-            for (int k = cur_n; k < KB; ++k) vp_step<C>(k, lane, lg_pos, vst);
+            for (int k = kstep; k < KB; ++k) vp_step<C>(k, lane, lg_pos, vst);
             vp_end<C>(sh, P_buf, P_off, P_n, lane, lg_pos, vst);
         }
         STAMP(1)
@@ -1284,7 +1401,12 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 while (m) {
                     const int jj = __ffsll((long long)m) - 1;
                     m &= m - 1;
-                    a1_query<C>(creg, sh.q[cur_buf][jj], sh.wrec[vwave][jj], vwave, lane);
+                    if ((prunedm >> jj) & 1ull) {  // still provably far: the exact record's lower bound
+                        const float lb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbp), jj));
+                        if (lane == 0) sh.wrec[vwave][jj].minbits = __float_as_uint(lb);
+                    } else {
+                        a1_query<C>(creg, sh.q[cur_buf][jj], sh.wrec[vwave][jj], vwave, lane);
+                    }
                 }
                 lds_barrier();
                 if constexpr (NWG == 2) {
@@ -1409,6 +1531,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         if (wave == 0) {  // publish this iteration's commits (earlier ones are in the registers)
             const bool fresh_e = lg_pos >= 0 && lg_tag == it;
             sh.pub_pos[lane] = fresh_e ? lg_pos : -1;
+            if (PRUNE && lane < KB) sh.ub[lane] = kInfBits;  // the next batch's bounds
         }
         lds_barrier();
         STAMP(4)
