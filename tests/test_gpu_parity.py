@@ -149,3 +149,29 @@ def test_knnfit_synthetic_ties(oracle, cs, r, n, eps, seed):
                                     want.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
     got = sc.knnfit_assign(fwd, q, eps)
     np.testing.assert_array_equal(got, want)
+
+
+# C4: the reference's lame_test corpus (tests/golden/lame_test, copied from the
+# reference as data) at -cs8 -cpf4096; expected digests from the oracle
+# (tests/golden/make_corpus.py)
+def _corpus():
+    import json
+    from golden.cases import HERE
+
+    return json.loads((HERE / "corpus_meta.json").read_text())
+
+
+@pytest.mark.parametrize("name", sorted(_corpus()["files"]))
+def test_corpus_matches_oracle(name):
+    import hashlib
+
+    import soundchunks_amd as sc
+    from golden.cases import HERE
+
+    meta = _corpus()
+    want = meta["files"][name]
+    wav = (HERE / "lame_test" / name).read_bytes()
+    assert hashlib.sha256(wav).hexdigest() == want["wav_sha256"]
+    got = sc.Encoder(meta["argv"]).encode(wav)
+    assert len(got) == want["gsc_bytes"]
+    assert hashlib.sha256(got).hexdigest() == want["gsc_sha256"]

@@ -139,3 +139,19 @@ def test_yakmo_seed_means_properties():
     # K >= N is rejected (the DLL would spin)
     assert lib.ora_yakmo_seed_means(4, D, x.ctypes.data_as(fp), 4, c.ctypes.data_as(fp),
                                     lab.ctypes.data_as(ctypes.POINTER(ctypes.c_int))) == -1
+
+
+@pytest.mark.parametrize("name", ["60.wav", "hihat.wav", "mstest.wav"])
+def test_oracle_reproduces_corpus_digest(name):
+    """The committed C4 digests (tests/golden/corpus_meta.json) are what the
+    oracle computes now (the three smallest corpus files, to stay fast)."""
+    import hashlib
+    import json
+
+    import oracle_ffi
+    from golden.cases import HERE
+
+    meta = json.loads((HERE / "corpus_meta.json").read_text())
+    wav = (HERE / "lame_test" / name).read_bytes()
+    gsc = oracle_ffi.encode(wav, meta["argv"], threads=8)
+    assert hashlib.sha256(gsc).hexdigest() == meta["files"][name]["gsc_sha256"]
