@@ -90,6 +90,15 @@ void gsc_parse_options(gsc_options *o, int argc, const char *const *argv);
  * *out is allocated by the library; release with gsc_free(). */
 int gsc_encode_wav(const uint8_t *wav, size_t wav_len, const gsc_options *o, uint8_t **out, size_t *out_len);
 
+/* Encode plus the reconstruction the reference builds after MakeFrames
+ * (encoder.lpr:2019-2031: TEncoder.MakeDstData, ComputePsyADelta, SaveWAV):
+ * *recon = the 16-bit signal the .gsc encodes, interleaved [sample][channel]
+ * over the padded SampleCount (*recon_len samples; free with gsc_free), as
+ * TEncoder.SaveWAV writes it (encoder.lpr:1154-1179); *psy_a_delta =
+ * ComputePsyADelta(srcData, dstData) (encoder.lpr:1862-1880).  Reconstruction
+ * and the PsyADelta sum run on the device. */
+int gsc_encode_wav_recon(const uint8_t *wav, size_t wav_len, const gsc_options *o, uint8_t **out, size_t *out_len,
+                         int16_t **recon, size_t *recon_len, double *psy_a_delta);
 /* Frame-range encode (multi-GPU sharding): runs the host pre-pass on the
  * whole file, encodes frames [frame_begin, frame_end) only and returns their
  * concatenated TFrame.SaveStream bytes; *frame_count = total frame count. */

@@ -792,8 +792,41 @@ static void frame_save(const enc_t *e, const frame_t *f, buf_t *o) {
     if (bit_cnt > 0) put16(o, bits & 0xffff);
 }
 
+/* make16BitSample (encoder.lpr:1638-1641): EnsureRange(round(smp * High(SmallInt))) */
+static int16_t make16(double smp) {
+    return (int16_t)clampll(fpc_round(smp * 32767.0), -32768, 32767);
+}
+
+/* Reconstruction of one frame (f4): TBand.MakeDstData (encoder.lpr:487-522;
+ * CBandCount = 1, underSample = 1, ChunkBlend = 0) writes each final chunk's
+ * CS samples, makeFloatSample of its reduced chunk (reversed / negated as
+ * KNNFit chose), at the channel's running position, dropping positions past
+ * the frame; TEncoder.MakeDstData (encoder.lpr:1518-1582) sums the (single)
+ * band into floatDst and stores make16BitSample.  recon is interleaved
+ * [sample][channel] over the padded SampleCount, as SaveWAV writes it
+ * (encoder.lpr:1154-1179). */
+static void frame_recon(const enc_t *e, const frame_t *f, int start, int sc, int16_t *recon) {
+    int CS = e->p.chunk_size, CH = e->channels, bd = e->p.chunk_bit_depth;
+    double law = 1.0 / (double)f->atten_div;
+    for (int i = 0; i < f->n; i++) {
+        int ch = i % CH, chunk = i / CH, c = f->red[i];
+        for (int j = 0; j < CS; j++) {
+            int pos = chunk * CS + j;
+            int16_t v = f->rdst[(size_t)c * CS + (f->rev[i] ? CS - 1 - j : j)];
+            double smp = ora_make_float_sample(v, bd, f->ratten[c], f->neg[i], law);
+            if (pos < sc) recon[(size_t)(start + pos) * CH + ch] = make16(0.0 + (0.0 + smp));
+        }
+    }
+}
+
 /* DoFrame (encoder.lpr:1433-1447) */
+static void do_frame_r(const enc_t *e, int fi, buf_t *o, frame_t *keep, reduce_trace *rtr, knn_trace *ktr,
+                       int16_t *recon);
 static void do_frame(const enc_t *e, int fi, buf_t *o, frame_t *keep, reduce_trace *rtr, knn_trace *ktr) {
+    do_frame_r(e, fi, o, keep, rtr, ktr, NULL);
+}
+static void do_frame_r(const enc_t *e, int fi, buf_t *o, frame_t *keep, reduce_trace *rtr, knn_trace *ktr,
+                       int16_t *recon) {
     frame_t f;
     memset(&f, 0, sizeof(f));
     int start = e->fr_start[fi], end = e->fr_end[fi];
@@ -811,6 +844,7 @@ static void do_frame(const enc_t *e, int fi, buf_t *o, frame_t *keep, reduce_tra
     frame_reduce(e, &f, rtr);
     frame_knnfit(e, &f, ktr);
     if (o) frame_save(e, &f, o);
+    if (recon) frame_recon(e, &f, start, sc, recon);
     if (keep) *keep = f;
     else frame_free(&f);
 }
@@ -818,6 +852,7 @@ static void do_frame(const enc_t *e, int fi, buf_t *o, frame_t *keep, reduce_tra
 typedef struct {
     const enc_t *e;
     buf_t *outs;
+    int16_t *recon; /* optional: interleaved reconstruction */
     int next, end;
     pthread_mutex_t mu;
 } pool_t;
@@ -829,7 +864,7 @@ static void *worker(void *arg) {
         int fi = pl->next++;
         pthread_mutex_unlock(&pl->mu);
         if (fi >= pl->end) break;
-        do_frame(pl->e, fi, &pl->outs[fi], NULL, NULL, NULL);
+        do_frame_r(pl->e, fi, &pl->outs[fi], NULL, NULL, NULL, pl->recon);
     }
     return NULL;
 }
@@ -838,8 +873,42 @@ static void *worker(void *arg) {
  * all); their TFrame.SaveStream bytes concatenated in frame order
  * (encoder.lpr:1181-1215 writes frames in order).  Used by the multi-rank
  * sharding tests: the concatenation over ranks equals ora_encode. */
+static int encode_frames_r(const uint8_t *wav, size_t wav_len, const gsc_params *p, int frame_begin, int frame_end,
+                           int threads, uint8_t **out, size_t *out_len, int *frame_count, int16_t **recon,
+                           size_t *recon_len, double *psy);
 int ora_encode_frames(const uint8_t *wav, size_t wav_len, const gsc_params *p, int frame_begin, int frame_end,
                       int threads, uint8_t **out, size_t *out_len, int *frame_count) {
+    return encode_frames_r(wav, wav_len, p, frame_begin, frame_end, threads, out, out_len, frame_count, NULL, NULL,
+                           NULL);
+}
+
+/* ComputePsyADelta (encoder.lpr:1862-1880) -> CompareEuclidean on Double
+ * arrays (encoder.lpr:1803-1814): sqrt(sum((src - dst)^2) / len), the sum
+ * sequential in channel-major order over the padded SampleCount. */
+static double psy_a_delta(const uint8_t *wav, size_t wav_len, int CH, int SC, const int16_t *recon) {
+    int psc = (int)((wav_len - 44) / (2 * (size_t)CH));
+    double acc = 0.0;
+    for (int j = 0; j < CH; j++)
+        for (int i = 0; i < SC; i++) {
+            int16_t s = 0;
+            if (i < psc) {
+                const uint8_t *b = wav + 44 + ((size_t)i * CH + j) * 2;
+                s = (int16_t)(b[0] | (b[1] << 8));
+            }
+            double d = (double)s - (double)recon[(size_t)i * CH + j];
+            acc += d * d;
+        }
+    return sqrt(acc / (double)((long long)CH * SC));
+}
+
+int ora_encode_recon(const uint8_t *wav, size_t wav_len, const gsc_params *p, int threads, uint8_t **out,
+                     size_t *out_len, int16_t **recon, size_t *recon_len, double *psy) {
+    return encode_frames_r(wav, wav_len, p, 0, -1, threads, out, out_len, NULL, recon, recon_len, psy);
+}
+
+static int encode_frames_r(const uint8_t *wav, size_t wav_len, const gsc_params *p, int frame_begin, int frame_end,
+                           int threads, uint8_t **out, size_t *out_len, int *frame_count, int16_t **recon,
+                           size_t *recon_len, double *psy) {
     enc_t e;
     memset(&e, 0, sizeof(e));
     e.p = *p;
@@ -863,6 +932,7 @@ int ora_encode_frames(const uint8_t *wav, size_t wav_len, const gsc_params *p, i
     pool_t pl;
     pl.e = &e;
     pl.outs = outs;
+    pl.recon = recon ? (int16_t *)calloc((size_t)e.sample_count * (size_t)e.channels + 1, sizeof(int16_t)) : NULL;
     pl.next = frame_begin;
     pl.end = frame_end;
     pthread_mutex_init(&pl.mu, NULL);
@@ -881,6 +951,11 @@ int ora_encode_frames(const uint8_t *wav, size_t wav_len, const gsc_params *p, i
         free(outs[i].b);
     }
     free(outs);
+    if (recon) {
+        *recon = pl.recon;
+        *recon_len = (size_t)e.sample_count * (size_t)e.channels;
+        if (psy) *psy = psy_a_delta(wav, wav_len, e.channels, e.sample_count, pl.recon);
+    }
     enc_free(&e);
     if (!all.b) all.b = (uint8_t *)malloc(1);
     *out = all.b;

@@ -53,6 +53,12 @@ void ora_parse_params(gsc_params *p, int argc, const char *const *argv);
 int ora_encode(const uint8_t *wav, size_t wav_len, const gsc_params *p, int threads, uint8_t **out,
                size_t *out_len);
 void ora_free(void *p);
+/* Full encode plus the reconstruction the reference builds after MakeFrames
+ * (f4: TBand/TEncoder.MakeDstData, encoder.lpr:487-522,1518-1582) as
+ * interleaved 16-bit samples over the padded SampleCount (SaveWAV order), and
+ * ComputePsyADelta(srcData, dstData) (encoder.lpr:1862-1880). */
+int ora_encode_recon(const uint8_t *wav, size_t wav_len, const gsc_params *p, int threads, uint8_t **out,
+                     size_t *out_len, int16_t **recon, size_t *recon_len, double *psy);
 /* Frames [frame_begin, frame_end) only (frame_end < 0 => all), concatenated
  * SaveStream bytes; *frame_count (may be NULL) = frames in the file. */
 int ora_encode_frames(const uint8_t *wav, size_t wav_len, const gsc_params *p, int frame_begin, int frame_end,

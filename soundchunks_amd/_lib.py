@@ -83,6 +83,10 @@ SIGNATURES = {
     "gsc_encode_wav_frames": (ctypes.c_int, [_U8P, ctypes.c_size_t, ctypes.POINTER(GscOptions), ctypes.c_int,
                                              ctypes.c_int, ctypes.POINTER(_U8P), ctypes.POINTER(ctypes.c_size_t),
                                              _IP]),
+    "gsc_encode_wav_recon": (ctypes.c_int, [_U8P, ctypes.c_size_t, ctypes.POINTER(GscOptions), ctypes.POINTER(_U8P),
+                                            ctypes.POINTER(ctypes.c_size_t),
+                                            ctypes.POINTER(ctypes.POINTER(ctypes.c_int16)),
+                                            ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_double)]),
     "gsc_count_frames": (ctypes.c_int, [_U8P, ctypes.c_size_t, ctypes.POINTER(GscOptions), _IP]),
     "gsc_prepare": (ctypes.c_void_p, [_U8P, ctypes.c_size_t, ctypes.POINTER(GscOptions)]),
     "gsc_prepared_frame_count": (ctypes.c_int, [ctypes.c_void_p]),

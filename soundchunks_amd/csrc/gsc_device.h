@@ -46,6 +46,15 @@ struct DspFrame {
     int32_t pad_;
 };
 
+// One frame of the reconstruction (TBand.MakeDstData, encoder.lpr:487-522).
+struct ReconFrame {
+    int64_t chunk_off;    // n chunk words (final reduced index << 2 | neg << 1 | rev) at +chunk_off
+    int64_t red_off;      // final reduced chunks: r*CS int16 at rdst + red_off*CS, attenuation at +red_off
+    int64_t out_off;      // the frame's first sample, relative to the batch's first sample
+    int32_t n, sc;        // chunkRefs count, frame sample count
+    double law;           // AttenuationLaw = 1 / AttenuationDivider
+};
+
 // One frame of TFrame.KNNFit (encoder.lpr:915-978).
 struct FitFrame {
     int64_t cand_off;     // R*CS floats: forward candidate values (neg/rev derived)

@@ -72,6 +72,19 @@ void warm_trig_tables(int cs);
 // idft sin (cs*cs f64 each), plus the DCT scale factors sqrt(1/2), sqrt(2/cs).
 void trig_pack(int cs, std::vector<double>* tab, double* s0, double* scale);
 
+// Reconstruction request of an encode: the 16-bit signal
+// the reference rebuilds after MakeFrames (encoder.lpr:2019-2027), written
+// into pcm (interleaved [sample][channel], the padded SampleCount), and the
+// exact integer sum of (srcData - dstData)^2 over the encoded frames (the
+// numerator of ComputePsyADelta, encoder.lpr:1862-1880).
+struct ReconOut {
+    int16_t* pcm = nullptr;
+    const uint8_t* wav = nullptr;  // the source WAV (srcData for PsyADelta)
+    size_t wav_len = 0;
+    unsigned long long sq = 0;
+    double ms = 0;
+};
+
 class Encoder {
    public:
     explicit Encoder(const gsc_options& o) : opt_(o) {}
@@ -84,7 +97,8 @@ class Encoder {
         return ((sc - 1) / opt_.chunk_size + 1) * channels_;
     }
     // Encode frames [b, e) and return their concatenated stream bytes
-    int encode_range(int b, int e, std::vector<uint8_t>* out, std::string* err, gsc_timing* tim);
+    int encode_range(int b, int e, std::vector<uint8_t>* out, std::string* err, gsc_timing* tim,
+                     ReconOut* recon = nullptr);
     // Device DSP of frame f alone (parity tests): attenuation divider and the
     // N x 2CS features
     int dsp_frame(int f, int* atten_div, std::vector<float>* feat, std::string* err);
@@ -99,6 +113,8 @@ class Encoder {
     // host side, features left in the device slab *dX at (*xoff)[i]
     int device_dsp(int b, std::vector<FrameState>& frames, void* dX, std::vector<int64_t>* xoff, double* ms,
                    std::string* err);
+    // reconstruction of frames [b, b + frames.size()) on the device (after KNNFit)
+    int device_recon(int b, const std::vector<FrameState>& frames, ReconOut* ro, std::string* err);
     void frame_reduce_post(FrameState& f, bool reduced) const;
     void frame_knnfit_post(FrameState& f) const;
     void frame_save(FrameState& f) const;

@@ -39,6 +39,11 @@ extern "C" hipError_t gsc_launch_features(int cs, const gsc::DspFrame* frames, i
                                           double scale, float* X, uint8_t* nr, hipStream_t st);
 extern "C" hipError_t gsc_launch_knnfit(int CS, gsc::FitFrame* frames, int nframes, int max_n, int max_r,
                                         const float* cand, const float* q, int* out, hipStream_t st);
+extern "C" hipError_t gsc_launch_recon(const gsc::ReconFrame* frames, int nframes, int max_n, int cs, int ch, int bd,
+                                       const uint32_t* chunk, const int16_t* rdst, const uint8_t* ratten, int16_t* out,
+                                       hipStream_t st);
+extern "C" hipError_t gsc_launch_sqdiff(const int16_t* a, const int16_t* b, int64_t n, unsigned long long* acc,
+                                        hipStream_t st);
 extern "C" hipError_t gsc_launch_ann_build_many(const void* trees, int ntrees, hipStream_t st);
 extern "C" hipError_t gsc_launch_knnfit_ann(const void* trees, const void* jobs, int njobs, const float* q, int* out,
                                             float* pq_key, void* pq_node, int pq_cap, hipStream_t st);
@@ -543,6 +548,73 @@ int Encoder::device_dsp(int b, std::vector<FrameState>& frames, void* dXv, std::
     return 0;
 }
 
+// ---- Encoder::device_recon: reconstruction + PsyADelta numerator (f4) -----
+int Encoder::device_recon(int b, const std::vector<FrameState>& frames, ReconOut* ro, std::string* err) {
+    const int cs = opt_.chunk_size, ch = channels_, nfr = int(frames.size());
+    if (nfr == 0) return 0;
+    const double t0 = now_ms();
+    const int64_t s_first = fr_start_[b], span = int64_t(fr_end_[b + nfr - 1]) - s_first + 1;
+    std::vector<ReconFrame> rf(static_cast<size_t>(nfr));
+    int64_t nchunk = 0, nred = 0;
+    int max_n = 0;
+    for (int i = 0; i < nfr; ++i) {
+        const FrameState& f = frames[i];
+        rf[i] = ReconFrame{nchunk, nred, int64_t(f.start) - s_first, f.n, f.sample_count, 1.0 / double(f.atten_div)};
+        nchunk += f.n;
+        nred += f.r;
+        max_n = std::max(max_n, f.n);
+    }
+    std::vector<uint32_t> words(static_cast<size_t>(nchunk));
+    std::vector<int16_t> rdst(static_cast<size_t>(std::max<int64_t>(nred, 1) * cs));
+    std::vector<uint8_t> ratten(static_cast<size_t>(std::max<int64_t>(nred, 1)));
+    parallel_for(nfr, host_threads(), [&](int i) {
+        const FrameState& f = frames[i];
+        uint32_t* w = words.data() + rf[i].chunk_off;
+        for (int c = 0; c < f.n; ++c) w[c] = uint32_t(f.red[c]) << 2 | uint32_t(f.neg[c] & 1) << 1 | uint32_t(f.rev[c] & 1);
+        std::copy(f.rdst.begin(), f.rdst.begin() + long(size_t(f.r) * cs), rdst.begin() + long(rf[i].red_off * cs));
+        std::copy(f.ratten.begin(), f.ratten.begin() + f.r, ratten.begin() + long(rf[i].red_off));
+    });
+    // srcData of the range (SmallInt, zero past the file's own samples: PrepareFrames pads, encoder.lpr:1317-1323)
+    const int64_t psc = ro->wav_len >= 44 ? int64_t((ro->wav_len - 44) / (2 * size_t(ch))) : 0;
+    std::vector<int16_t> src(static_cast<size_t>(span * ch), 0);
+    const int64_t avail = std::max<int64_t>(0, std::min(span, psc - s_first));
+    if (avail > 0) std::memcpy(src.data(), ro->wav + 44 + size_t(s_first) * ch * 2, size_t(avail) * ch * 2);
+    DevBuf<ReconFrame> dF;
+    DevBuf<uint32_t> dW;
+    DevBuf<int16_t> dR, dOut, dSrc;
+    DevBuf<uint8_t> dA;
+    DevBuf<unsigned long long> dAcc;
+    auto chk = [&](hipError_t r, const char* what) {
+        if (r == hipSuccess) return true;
+        *err = std::string("reconstruction: ") + what + ": " + hipGetErrorString(r);
+        return false;
+    };
+    const size_t nout = size_t(span) * ch;
+    if (!chk(dF.alloc(size_t(nfr)), "alloc") || !chk(dW.alloc(words.size()), "alloc") ||
+        !chk(dR.alloc(rdst.size()), "alloc") || !chk(dA.alloc(ratten.size()), "alloc") ||
+        !chk(dOut.alloc(nout), "alloc") || !chk(dSrc.alloc(nout), "alloc") || !chk(dAcc.alloc(1), "alloc"))
+        return -1;
+    if (!chk(hipMemcpy(dF.p, rf.data(), sizeof(ReconFrame) * rf.size(), hipMemcpyHostToDevice), "upload") ||
+        !chk(hipMemcpy(dW.p, words.data(), sizeof(uint32_t) * words.size(), hipMemcpyHostToDevice), "upload") ||
+        !chk(hipMemcpy(dR.p, rdst.data(), sizeof(int16_t) * rdst.size(), hipMemcpyHostToDevice), "upload") ||
+        !chk(hipMemcpy(dA.p, ratten.data(), ratten.size(), hipMemcpyHostToDevice), "upload") ||
+        !chk(hipMemcpy(dSrc.p, src.data(), sizeof(int16_t) * nout, hipMemcpyHostToDevice), "upload") ||
+        !chk(hipMemset(dOut.p, 0, sizeof(int16_t) * nout), "memset") ||  // dstData starts zeroed (encoder.lpr:497-501)
+        !chk(hipMemset(dAcc.p, 0, sizeof(unsigned long long)), "memset") ||
+        !chk(gsc_launch_recon(dF.p, nfr, max_n, cs, ch, opt_.chunk_bit_depth, dW.p, dR.p, dA.p, dOut.p, nullptr),
+             "recon launch") ||
+        !chk(gsc_launch_sqdiff(dSrc.p, dOut.p, int64_t(nout), dAcc.p, nullptr), "PsyADelta launch"))
+        return -1;
+    unsigned long long sq = 0;
+    if (!chk(hipMemcpy(ro->pcm + size_t(s_first) * ch, dOut.p, sizeof(int16_t) * nout, hipMemcpyDeviceToHost),
+             "download") ||
+        !chk(hipMemcpy(&sq, dAcc.p, sizeof(sq), hipMemcpyDeviceToHost), "download"))
+        return -1;
+    ro->sq += sq;
+    ro->ms += now_ms() - t0;
+    return 0;
+}
+
 int Encoder::dsp_frame(int fi, int* atten_div, std::vector<float>* feat, std::string* err) {
     if (ensure_device() != 0) {
         *err = t_err;
@@ -571,7 +643,8 @@ int Encoder::dsp_frame(int fi, int* atten_div, std::vector<float>* feat, std::st
 }
 
 // ---- Encoder::encode_range: host srcData, device DSP + hot path ------------
-int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* err, gsc_timing* tim) {
+int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* err, gsc_timing* tim,
+                          ReconOut* recon) {
     if (ensure_device() != 0) {
         *err = t_err;
         return -1;
@@ -680,6 +753,7 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
         frame_knnfit_post(frames[i]);
         frame_save(frames[i]);
     });
+    if (recon && device_recon(b, frames, recon, err) != 0) return -1;
     out->clear();
     for (auto& f : frames) out->insert(out->end(), f.stream.begin(), f.stream.end());
     double t4 = now_ms();
@@ -883,6 +957,58 @@ int gsc_frame_dsp(const uint8_t* wav, size_t wav_len, const gsc_options* o, int 
 
 int gsc_encode_wav(const uint8_t* wav, size_t wav_len, const gsc_options* o, uint8_t** out, size_t* out_len) {
     return gsc_encode_wav_frames(wav, wav_len, o, 0, -1, out, out_len, nullptr);
+}
+
+int gsc_encode_wav_recon(const uint8_t* wav, size_t wav_len, const gsc_options* o, uint8_t** out, size_t* out_len,
+                         int16_t** recon, size_t* recon_len, double* psy_a_delta) {
+    if (!wav || !o || !out || !out_len || !recon || !recon_len || !psy_a_delta)
+        return fail("gsc_encode_wav_recon: null argument");
+    *out = nullptr;
+    *recon = nullptr;
+    const double t0 = now_ms();
+    Encoder enc(*o);
+    std::string err;
+    if (enc.prepare(wav, wav_len, &err) != 0) return fail(err);
+    const int ch = enc.channels();
+    const size_t n = size_t(enc.sample_count()) * size_t(ch);
+    ReconOut ro;
+    ro.pcm = static_cast<int16_t*>(std::calloc(std::max<size_t>(n, 1), sizeof(int16_t)));
+    if (!ro.pcm) return fail("out of host memory");
+    ro.wav = wav;
+    ro.wav_len = wav_len;
+    std::vector<uint8_t> bytes;
+    const int fc = enc.frame_count();
+    if (fc > 0 && enc.encode_range(0, fc, &bytes, &err, &t_tim, &ro) != 0) {
+        std::free(ro.pcm);
+        return fail(err);
+    }
+    *out = static_cast<uint8_t*>(std::malloc(std::max<size_t>(bytes.size(), 1)));
+    if (!*out) {
+        std::free(ro.pcm);
+        return fail("out of host memory");
+    }
+    if (!bytes.empty()) std::memcpy(*out, bytes.data(), bytes.size());
+    *out_len = bytes.size();
+    // ComputePsyADelta = CompareEuclidean over Double copies (encoder.lpr:1803-1814,1862-1880): every
+    // partial sum is an integer, exact in f64 below 2^53, where it equals the device's exact sum
+    double acc = 0.0;
+    if (ro.sq < (1ull << 53)) {
+        acc = double(ro.sq);
+    } else {  // the reference's sequential f64 sum, channel-major
+        const size_t psc = wav_len >= 44 ? (wav_len - 44) / (2 * size_t(ch)) : 0;
+        for (int j = 0; j < ch; ++j)
+            for (size_t i = 0; i < size_t(enc.sample_count()); ++i) {
+                int16_t sv = 0;
+                if (i < psc) std::memcpy(&sv, wav + 44 + (i * ch + j) * 2, 2);
+                const double d = double(sv) - double(ro.pcm[i * ch + j]);
+                acc += d * d;
+            }
+    }
+    *psy_a_delta = n ? std::sqrt(acc / double(n)) : 0.0;
+    *recon = ro.pcm;
+    *recon_len = n;
+    t_tim.total_ms = now_ms() - t0;
+    return 0;
 }
 
 int gsc_yakmo_seed_means(int n, int d, const float* x, int k, float* centroids) {

@@ -67,6 +67,26 @@ class Encoder:
         finally:
             lib.gsc_free(out)
 
+    def encode_recon(self, wav: bytes):
+        """Encode, plus the reference's reconstruction and PsyADelta
+        (encoder.lpr:2019-2031): (.gsc bytes, int16 samples interleaved
+        [sample][channel] over the padded SampleCount, PsyADelta)."""
+        lib = _lib.load()
+        arr, ptr = _u8(wav)
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_size_t(0)
+        rec = ctypes.POINTER(ctypes.c_int16)()
+        rn = ctypes.c_size_t(0)
+        psy = ctypes.c_double(0.0)
+        rc = lib.gsc_encode_wav_recon(ptr, len(arr), ctypes.byref(self.options), ctypes.byref(out), ctypes.byref(n),
+                                      ctypes.byref(rec), ctypes.byref(rn), ctypes.byref(psy))
+        _lib.check(rc)
+        try:
+            return (ctypes.string_at(out, n.value), np.ctypeslib.as_array(rec, (rn.value,)).copy(), psy.value)
+        finally:
+            lib.gsc_free(out)
+            lib.gsc_free(rec)
+
     def prepare(self, wav: bytes) -> "Prepared":
         """Load + PrepareFrames once (the frame boundaries of the whole file)."""
         return Prepared(self, wav)

@@ -64,6 +64,11 @@ def load():
                                           ctypes.c_int, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t),
                                           ctypes.POINTER(ctypes.c_int)]
         lib.ora_encode_frames.restype = ctypes.c_int
+        lib.ora_encode_recon.argtypes = [u8p, ctypes.c_size_t, ctypes.POINTER(OraParams), ctypes.c_int,
+                                         ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t),
+                                         ctypes.POINTER(ctypes.POINTER(ctypes.c_int16)),
+                                         ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_double)]
+        lib.ora_encode_recon.restype = ctypes.c_int
         lib.ora_free.argtypes = [ctypes.c_void_p]
         lib.ora_get_stats.argtypes = [ctypes.POINTER(OraStats)]
         lib.ora_trace_frame.argtypes = [u8p, ctypes.c_size_t, ctypes.POINTER(OraParams), ctypes.c_int,
@@ -118,6 +123,27 @@ def encode(wav: bytes, argv=(), threads: int = 1) -> bytes:
         return ctypes.string_at(out, n.value)
     finally:
         lib.ora_free(out)
+
+
+def encode_recon(wav: bytes, argv=(), threads: int = 1):
+    """(.gsc bytes, reconstruction int16 [samples x channels] interleaved, PsyADelta)."""
+    lib = load()
+    p = params(argv)
+    a, ptr = _u8(wav)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t(0)
+    rec = ctypes.POINTER(ctypes.c_int16)()
+    rn = ctypes.c_size_t(0)
+    psy = ctypes.c_double(0.0)
+    rc = lib.ora_encode_recon(ptr, len(a), ctypes.byref(p), threads, ctypes.byref(out), ctypes.byref(n),
+                              ctypes.byref(rec), ctypes.byref(rn), ctypes.byref(psy))
+    if rc != 0:
+        raise RuntimeError(f"oracle encode failed: {rc}")
+    try:
+        return (ctypes.string_at(out, n.value), np.ctypeslib.as_array(rec, (rn.value,)).copy(), psy.value)
+    finally:
+        lib.ora_free(out)
+        lib.ora_free(rec)
 
 
 def encode_frames(wav: bytes, argv=(), frame_begin: int = 0, frame_end: int = -1, threads: int = 1):

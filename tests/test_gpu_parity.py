@@ -175,3 +175,18 @@ def test_corpus_matches_oracle(name):
     got = sc.Encoder(meta["argv"]).encode(wav)
     assert len(got) == want["gsc_bytes"]
     assert hashlib.sha256(got).hexdigest() == want["gsc_sha256"]
+
+
+# f4: reconstruction (TBand/TEncoder.MakeDstData) and PsyADelta on the device
+@pytest.mark.parametrize("name", ["c1_test_cs8_cpf256", "hihat_cs4_default", "syn3s_cs8_cpf1000_cbd12",
+                                  "syn8s_c3_cs16_cpf4096_cbd12", "tiny_passthrough_cs8", "quiet_tone_cs8_cpf1024"])
+def test_reconstruction_matches_oracle(oracle, name):
+    import soundchunks_amd as sc
+
+    make, argv = CASES[name]
+    wav = make()
+    gsc, rec, psy = sc.Encoder(argv).encode_recon(wav)
+    ogsc, orec, opsy = oracle.encode_recon(wav, argv, threads=8)
+    assert gsc == ogsc == golden_path(name).read_bytes()
+    np.testing.assert_array_equal(rec, orec)
+    assert psy == opsy  # bit-identical f64

@@ -155,3 +155,24 @@ def test_oracle_reproduces_corpus_digest(name):
     wav = (HERE / "lame_test" / name).read_bytes()
     gsc = oracle_ffi.encode(wav, meta["argv"], threads=8)
     assert hashlib.sha256(gsc).hexdigest() == meta["files"][name]["gsc_sha256"]
+
+
+@pytest.mark.parametrize("name", ["c1_test_cs8_cpf256", "hihat_cs8_cpf256", "syn2s_c2_cs8_cpf4096"])
+def test_oracle_reconstruction_agrees_with_decoder(name):
+    """f4 pin: the encoder-side reconstruction (encoder.lpr:487-522,1518-1582)
+    and the independently restated decoder (decoder.lpr:37-220) rebuild the
+    same signal from the same .gsc, up to the decoder's integer lookup
+    arithmetic (12-bit rescale, 15-bit attenuation table)."""
+    make, argv = CASES[name]
+    wav = make()
+    gsc, rec, psy = oracle_ffi.encode_recon(wav, argv, threads=8)
+    assert gsc == golden_path(name).read_bytes()
+    pcm = np.asarray(oracle_ffi.decode(gsc)[0]).ravel().astype(np.int64)
+    k = min(len(pcm), len(rec))
+    assert k >= len(rec) - 64 * 2
+    diff = np.abs(pcm[:k] - rec[:k].astype(np.int64))
+    assert diff.max() <= 32
+    src = np.zeros(len(rec))  # srcData padded with zeros to the block multiple (encoder.lpr:1317-1323)
+    s = np.frombuffer(wav[44:44 + (len(wav) - 44) // 2 * 2], dtype="<i2").astype(np.float64)[:len(rec)]
+    src[:len(s)] = s
+    assert psy == pytest.approx(np.sqrt(((src - rec) ** 2).sum() / len(rec)), rel=1e-12)
