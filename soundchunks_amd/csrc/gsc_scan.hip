@@ -1584,27 +1584,11 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                     for (int i = tid; i < C::KG; i += nthreads)
                         sh.dist[(1 - wg) * C::KG + i] = __uint_as_float(xget(xp, i));
                 }
-                // the centroid registers wait in C (pass-start copy, rewritten at pass end)
-                // so the DFS has the register file
-#pragma unroll
-                for (int s = 0; s < SL; ++s)
-                    if (p0 + s < K) {
-                        const int id = sh.t.pidx[p0 + s];
-#pragma unroll
-                        for (int d = 0; d < D; ++d) C_[(int64_t)id * D + d] = creg[s][d];
-                    }
-                __asm__ volatile("" ::: "memory");  // the reload below must not be forwarded from the stores
+                // the centroid registers stay live across the DFS (it needs ~40 more
+                // VGPRs; parking the 128 in C and reloading them cost 2x the DFS time)
                 lds_barrier();  // sh.dist complete
                 dfs_parallel<C>(sh, tid, lane, wave, bpos, key);
                 bpos = uniform_int(bpos);
-                __asm__ volatile("" ::: "memory");
-#pragma unroll
-                for (int s = 0; s < SL; ++s)
-                    if (p0 + s < K) {
-                        const int id = sh.t.pidx[p0 + s];
-#pragma unroll
-                        for (int d = 0; d < D; ++d) creg[s][d] = C_[(int64_t)id * D + d];
-                    }
                 ++slow_total;
                 STAMP(11)
             }
