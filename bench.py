@@ -35,7 +35,7 @@ CONFIGS = {
 
 VALU_F32_PEAK_TOPS = 78.6  # non-fused f32 VALU ops/s: half the 157.3 TFLOPS FMA-counted peak
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md (spec)
-PMC_SUMMARY = ROOT / "profiles" / "r01" / "pmc_summary.json"  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
+PMC_SUMMARY = ROOT / "profiles" / "r02" / "pmc_summary.json"  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
 
 
 def _dist_env():
@@ -187,7 +187,11 @@ def main():
     # rocprofv3 summary, gfx950-corrected) x frames in this launch
     traffic = None
     if PMC_SUMMARY.exists():
-        kern = json.loads(PMC_SUMMARY.read_text())["kernels"].get(f"gsc::scan_batch_kernel<{2 * cs}, 12>")
+        ks = json.loads(PMC_SUMMARY.read_text())["kernels"]
+        # the scan kernel's instance at this D and K = 4096 (ScanCfg<D, 12, slots, CUs>)
+        kern = next((v for k, v in ks.items()
+                     if k.startswith("gsc::scan_batch_kernel") and (f"<{2 * cs}, 12," in k or f"<{2 * cs}, 12>" in k)),
+                    None)
         if kern:
             traffic = kern["hbm_bytes_per_frame_per_launch"] * tm["reduce_frames"]
     result = {

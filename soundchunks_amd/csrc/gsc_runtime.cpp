@@ -697,10 +697,11 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
             slow += sl[j];
         }
     }
-    double t2 = now_ms();
+    double t2 = now_ms(), t2c = 0;
     std::vector<char> is_red(size_t(nfr), 0);
     for (int i : red_idx) is_red[i] = 1;
     parallel_for(nfr, host_threads(), [&](int i) { frame_reduce_post(frames[i], is_red[i] != 0); });
+    const double t2b = now_ms();
     // --- KNNFit on the device
     {
         std::vector<int> Rs(static_cast<size_t>(nfr)), Nq(static_cast<size_t>(nfr));
@@ -738,6 +739,7 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
             for (size_t k = 0; k < f.src.size(); ++k) qp[k] = float(f.src[k]);
         });
         std::vector<int> best;
+        t2c = now_ms();
         if (run_knnfit_batch(cs, Rs, Nq, eps, cand, q, &best, &knn_ms) != 0) {
             *err = t_err;
             return -1;
@@ -757,6 +759,11 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
     out->clear();
     for (auto& f : frames) out->insert(out->end(), f.stream.begin(), f.stream.end());
     double t4 = now_ms();
+    if (std::getenv("GSC_HOST_TIMING"))
+        std::fprintf(stderr,
+                     "host timing [ms]: frames+dsp %.1f (dsp %.1f) | reduce (yakmo %.1f scan %.1f) %.1f | reduce_post %.1f |"
+                     " knn_stage %.1f | knnfit call %.1f (kernel %.1f) | knn_post+save+concat %.1f\n",
+                     t1 - t0, dsp_ms, yak_ms, scan_ms, t2 - t1, t2b - t2, t2c - t2b, t3 - t2c, knn_ms, t4 - t3);
     if (tim) {
         tim->host_frames_ms = t1 - t0 - dsp_ms;
         tim->gpu_dsp_ms = dsp_ms;
