@@ -129,6 +129,9 @@ int gsc_frame_dsp(const uint8_t *wav, size_t wav_len, const gsc_options *o, int 
 /* Stage entry points on host buffers (row-major), used by parity tests. */
 int gsc_yakmo_seed_means(int n, int d, const float *x, int k, float *centroids);
 int gsc_scan_reduce(int n, int d, const float *x, int k, float *centroids, int *clusters, int precision, int *iters);
+/* -py reducer stage (cluster.py Birch labels, extern.pas:350-437): n x d
+ * Single features of one frame -> labels[n] in [0, k). */
+int gsc_birch_labels(int n, int d, const float *x, int k, int *labels);
 int gsc_knnfit_assign(int r, int cs, const float *cand_fwd, int n, const float *q, float eps, int *best);
 
 /* Timing of the last gsc_encode_* call on the calling thread (milliseconds),

@@ -53,6 +53,9 @@ void ora_parse_params(gsc_params *p, int argc, const char *const *argv);
 int ora_encode(const uint8_t *wav, size_t wav_len, const gsc_params *p, int threads, uint8_t **out,
                size_t *out_len);
 void ora_free(void *p);
+/* -py mode: the per-frame labels cluster.py returned (tests/golden/birch_*),
+ * labels of frame f at labels + frame_offsets[f]; NULL clears. */
+void ora_set_py_labels(const int *labels, const long long *frame_offsets, int nframes);
 /* Full encode plus the reconstruction the reference builds after MakeFrames
  * (f4: TBand/TEncoder.MakeDstData, encoder.lpr:487-522,1518-1582) as
  * interleaved 16-bit samples over the padded SampleCount (SaveWAV order), and

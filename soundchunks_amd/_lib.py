@@ -99,6 +99,7 @@ SIGNATURES = {
                                      ctypes.POINTER(_FP), _IP]),
     "gsc_yakmo_seed_means": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _FP, ctypes.c_int, _FP]),
     "gsc_scan_reduce": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _FP, ctypes.c_int, _FP, _IP, ctypes.c_int, _IP]),
+    "gsc_birch_labels": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _FP, ctypes.c_int, _IP]),
     "gsc_knnfit_assign": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _FP, ctypes.c_int, _FP, ctypes.c_float, _IP]),
     "gsc_last_timing": (None, [ctypes.POINTER(GscTiming)]),
     "gsc_device_count": (ctypes.c_int, []),

@@ -166,10 +166,6 @@ int Encoder::prepare(const uint8_t* wav, size_t len, std::string* err) {
         *err = "ChunkBlend != 0 is not supported (decoder.lpr asserts it is 0)";
         return -2;
     }
-    if (o.python_reduce) {
-        *err = "-py (cluster.py Birch reducer) is not part of the GPU path";
-        return -2;
-    }
     if (!(o.chunk_bit_depth == 8 || o.chunk_bit_depth == 12)) {
         *err = "ChunkBitDepth must be 8 or 12 (TFrame.SaveStream)";
         return -2;

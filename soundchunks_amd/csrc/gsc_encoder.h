@@ -85,6 +85,9 @@ struct ReconOut {
     double ms = 0;
 };
 
+// -py reducer (gsc_birch_host.cpp): cluster.py's Birch labels of N samples
+int birch_reduce_labels(int n, int d, const float* feat, int K, int* labels, std::string* err);
+
 class Encoder {
    public:
     explicit Encoder(const gsc_options& o) : opt_(o) {}

@@ -677,7 +677,25 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
         }
     double yak_ms = 0, scan_ms = 0, knn_ms = 0;
     long long passes = 0, slow = 0, restarts = 0;
-    if (!red_idx.empty()) {
+    if (!red_idx.empty() && opt_.python_reduce) {
+        // -py: TFrame.Reduce with PythonReduce (encoder.lpr:837-841): Birch labels
+        // (gsc_birch_host.cpp), no yakmo and no KNNScanReduce
+        const double tb = now_ms();
+        for (size_t j = 0; j < red_idx.size(); ++j) {
+            FrameState& f = frames[red_idx[j]];
+            std::vector<float> x(size_t(f.n) * D);
+            if (hipMemcpy(x.data(), dFeat.p + red_xoff[j], sizeof(float) * x.size(), hipMemcpyDeviceToHost) !=
+                hipSuccess) {
+                *err = "-py: feature download failed";
+                return -1;
+            }
+            f.clusters.resize(size_t(f.n));
+            if (birch_reduce_labels(f.n, D, x.data(), K, f.clusters.data(), err) != 0) return -1;
+            f.scan_iters = 0;
+            f.scan_slow = 0;
+        }
+        scan_ms += now_ms() - tb;
+    } else if (!red_idx.empty()) {
         std::vector<float> C;
         std::vector<int> cl, it, sl;
         g_scan_rounds.store(0);
@@ -1097,6 +1115,14 @@ int gsc_scan_reduce(int n, int d, const float* x, int k, float* centroids, int* 
         }
         std::fprintf(stderr, "\n");
     }
+    return 0;
+}
+
+int gsc_birch_labels(int n, int d, const float* x, int k, int* labels) {
+    if (!x || !labels || n <= 0 || d <= 0 || k <= 0) return fail("gsc_birch_labels: invalid argument");
+    if (ensure_device() != 0) return -1;
+    std::string err;
+    if (birch_reduce_labels(n, d, x, k, labels, &err) != 0) return fail(err);
     return 0;
 }
 

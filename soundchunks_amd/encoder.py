@@ -173,6 +173,15 @@ def scan_reduce(x: np.ndarray, c0: np.ndarray, precision: int = 3):
     return c, cl, it.value
 
 
+def birch_labels(x: np.ndarray, k: int) -> np.ndarray:
+    """-py reducer stage: Birch labels of one frame's features (gsc_birch_host.cpp)."""
+    lib = _lib.load()
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.zeros(x.shape[0], dtype=np.int32)
+    _lib.check(lib.gsc_birch_labels(x.shape[0], x.shape[1], _fp(x), k, _ip(out)))
+    return out
+
+
 def knnfit_assign(cand_fwd: np.ndarray, q: np.ndarray, eps: float) -> np.ndarray:
     """KNNFit candidate choice f = 4c + 2neg + rev per query on the GPU."""
     cand_fwd = np.ascontiguousarray(cand_fwd, dtype=np.float32)

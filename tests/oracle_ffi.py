@@ -69,6 +69,7 @@ def load():
                                          ctypes.POINTER(ctypes.POINTER(ctypes.c_int16)),
                                          ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_double)]
         lib.ora_encode_recon.restype = ctypes.c_int
+        lib.ora_set_py_labels.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         lib.ora_free.argtypes = [ctypes.c_void_p]
         lib.ora_get_stats.argtypes = [ctypes.POINTER(OraStats)]
         lib.ora_trace_frame.argtypes = [u8p, ctypes.c_size_t, ctypes.POINTER(OraParams), ctypes.c_int,
@@ -123,6 +124,24 @@ def encode(wav: bytes, argv=(), threads: int = 1) -> bytes:
         return ctypes.string_at(out, n.value)
     finally:
         lib.ora_free(out)
+
+
+_py_keep = None
+
+
+def set_py_labels(labels=None, offsets=None):
+    """-py mode: per-frame cluster.py labels (concatenated, int32) and each
+    frame's offset into them (int64); None clears."""
+    global _py_keep
+    lib = load()
+    if labels is None:
+        _py_keep = None
+        lib.ora_set_py_labels(None, None, 0)
+        return
+    lab = np.ascontiguousarray(labels, dtype=np.int32)
+    off = np.ascontiguousarray(offsets, dtype=np.int64)
+    _py_keep = (lab, off)
+    lib.ora_set_py_labels(lab.ctypes.data, off.ctypes.data, len(off))
 
 
 def encode_recon(wav: bytes, argv=(), threads: int = 1):

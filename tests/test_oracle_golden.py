@@ -176,3 +176,50 @@ def test_oracle_reconstruction_agrees_with_decoder(name):
     s = np.frombuffer(wav[44:44 + (len(wav) - 44) // 2 * 2], dtype="<i2").astype(np.float64)[:len(rec)]
     src[:len(s)] = s
     assert psy == pytest.approx(np.sqrt(((src - rec) ** 2).sum() / len(rec)), rel=1e-12)
+
+
+# a9 (-py): the oracle fed cluster.py's labels reproduces the committed .gsc,
+# and the datasets it hands cluster.py are the fixtures' (make_birch.py)
+def test_oracle_python_reduce_reproduces_fixture():
+    import json
+
+    from golden.cases import HERE
+
+    want = json.loads((HERE / "golden_meta.json").read_text())["mstest_fl500_cpf256_py"]
+    z = np.load(HERE / "birch_file_mstest_fl500_cpf256_py.npz")
+    wav = (HERE / "lame_test" / "mstest.wav").read_bytes()
+    oracle_ffi.set_py_labels(z["labels"], z["offsets"])
+    try:
+        got = oracle_ffi.encode(wav, want["argv"], threads=8)
+    finally:
+        oracle_ffi.set_py_labels(None)
+    assert got == (HERE / "mstest_fl500_cpf256_py.gsc").read_bytes()
+    for name in ("mstest_fl500_f0", "mstest_fl500_f2"):
+        b = np.load(HERE / f"birch_{name}.npz")
+        tr = oracle_ffi.trace_frame(wav, [str(a) for a in b["argv"]], int(b["frame"]))
+        np.testing.assert_array_equal(np.asarray(tr["dataset"], np.float32), b["dataset"])
+        assert int(tr["K"]) == int(b["k"])
+
+
+# the -py reducer's host part (gsc_birch_host.cpp: CF tree, linkage labelling,
+# _hc_cut) with host restatements of its two device steps (tools/birch), built
+# with g++ here, against cluster.py's labels
+@pytest.mark.parametrize("name", ["mstest_fl500_f0", "mstest_fl500_f2"])
+def test_birch_host_part_matches_cluster_py(tmp_path, name):
+    import subprocess
+    from pathlib import Path
+
+    from golden.cases import HERE
+
+    root = Path(__file__).resolve().parents[1]
+    so = tmp_path / "birch_host.so"
+    subprocess.run(["g++", "-O2", "-ffp-contract=off", "-shared", "-fPIC", "-o", str(so),
+                    str(root / "tools" / "birch" / "host_check.cpp"),
+                    str(root / "soundchunks_amd" / "csrc" / "gsc_birch_host.cpp")], check=True)
+    lib = ctypes.CDLL(str(so))
+    z = np.load(HERE / f"birch_{name}.npz")
+    x = np.ascontiguousarray(z["dataset"], np.float32)
+    out = np.zeros(x.shape[0], np.int32)
+    assert lib.birch_host_labels(x.shape[0], x.shape[1], ctypes.c_void_p(x.ctypes.data), int(z["k"]),
+                                 ctypes.c_void_p(out.ctypes.data)) == 0
+    np.testing.assert_array_equal(out, z["labels"])
