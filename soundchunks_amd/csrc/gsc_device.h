@@ -31,6 +31,7 @@ struct ReduceFrame {
     int32_t loop_iters;   // out: batched-pipeline iterations (diagnostic); -1 = guard tripped
     int32_t tree_exact;   // out: passes whose kd-tree needed the sequential build (median ties)
     int32_t xseq;         // two-CU frames (D = 32, K = 4096): tag of the last hand-off between the two CUs
+    uint64_t t_done;      // out: s_memrealtime (100 MHz) when the batched kernel finished the frame
     uint64_t stamps[128]; // out (GSC_STAMPS builds only): per-phase cycles, 16 per wave
 };
 

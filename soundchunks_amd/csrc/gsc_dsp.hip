@@ -113,7 +113,8 @@ template <int CS>
 __global__ __launch_bounds__(256) void features_kernel(const DspFrame* __restrict__ frames, int nframes,
                                                        const double* __restrict__ samp, int64_t span, int ch,
                                                        const double* __restrict__ trig_g, double s0, double scale,
-                                                       float* __restrict__ X, uint8_t* __restrict__ nr) {
+                                                       float* __restrict__ X, uint8_t* __restrict__ nr,
+                                                       float* __restrict__ Q) {
     __shared__ double tr[5 * CS * CS];
     for (int i = threadIdx.x; i < 5 * CS * CS; i += blockDim.x) tr[i] = trig_g[i];
     __syncthreads();
@@ -153,6 +154,11 @@ __global__ __launch_bounds__(256) void features_kernel(const DspFrame* __restric
     for (int k = CS / 2; k < CS; ++k) p2 += fabs(s[k]);
     const bool rev = p1 > p2;
     nr[fr.c_off + c] = (uint8_t)((neg ? 1 : 0) | (rev ? 2 : 0));
+    if (Q) {  // KNNFit queries: Single(srcData) (encoder.lpr:945-948)
+        float* qo = Q + (fr.c_off + c) * CS;
+#pragma unroll
+        for (int k = 0; k < CS; ++k) qo[k] = float(s[k]);
+    }
     double data[CS], temp[CS];
 #pragma unroll
     for (int k = 0; k < CS; ++k) data[k] = s[rev ? CS - 1 - k : k] * (neg ? -1.0 : 1.0);
@@ -194,10 +200,30 @@ __global__ __launch_bounds__(256) void features_kernel(const DspFrame* __restric
     }
 }
 
+// TEncoder.Load's sample conversion (encoder.lpr:1111-1152): SmallInt / 32767
+// into the planar f64 slab the DSP kernels read; pcm = [sample][ch] of the span
+__global__ __launch_bounds__(256) void pcm_kernel(const int16_t* __restrict__ pcm, int64_t span, int ch,
+                                                  double* __restrict__ samp) {
+    const int64_t total = span * ch;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = p / ch;
+        const int j = (int)(p - t * ch);
+        samp[(int64_t)j * span + t] = (double)pcm[p] / 32767.0;
+    }
+}
+
 }  // namespace
 }  // namespace gsc
 
 using namespace gsc;
+
+extern "C" hipError_t gsc_launch_pcm(const int16_t* pcm, int64_t span, int ch, double* samp, hipStream_t st) {
+    const int64_t total = span * ch;
+    const int64_t blocks = (total + 255) / 256;
+    hipLaunchKernelGGL(pcm_kernel, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, st, pcm, span, ch,
+                       samp);
+    return hipGetLastError();
+}
 
 // FindAttenuationDivider for every frame (one wave per frame)
 extern "C" hipError_t gsc_launch_atten(int cs, DspFrame* frames, int nframes, const double* samp, int64_t span, int ch,
@@ -214,12 +240,12 @@ extern "C" hipError_t gsc_launch_atten(int cs, DspFrame* frames, int nframes, co
 // chunk features for every frame; trig = 5 CS x CS f64 tables (dct, dft cos/sin, idft cos/sin)
 extern "C" hipError_t gsc_launch_features(int cs, const DspFrame* frames, int nframes, int max_n, const double* samp,
                                           int64_t span, int ch, const double* trig, double s0, double scale, float* X,
-                                          uint8_t* nr, hipStream_t st) {
+                                          uint8_t* nr, float* Q, hipStream_t st) {
     const dim3 grid((max_n + 255) / 256, nframes), block(256);
     switch (cs) {
-    case 4: hipLaunchKernelGGL(features_kernel<4>, grid, block, 0, st, frames, nframes, samp, span, ch, trig, s0, scale, X, nr); break;
-    case 8: hipLaunchKernelGGL(features_kernel<8>, grid, block, 0, st, frames, nframes, samp, span, ch, trig, s0, scale, X, nr); break;
-    case 16: hipLaunchKernelGGL(features_kernel<16>, grid, block, 0, st, frames, nframes, samp, span, ch, trig, s0, scale, X, nr); break;
+    case 4: hipLaunchKernelGGL(features_kernel<4>, grid, block, 0, st, frames, nframes, samp, span, ch, trig, s0, scale, X, nr, Q); break;
+    case 8: hipLaunchKernelGGL(features_kernel<8>, grid, block, 0, st, frames, nframes, samp, span, ch, trig, s0, scale, X, nr, Q); break;
+    case 16: hipLaunchKernelGGL(features_kernel<16>, grid, block, 0, st, frames, nframes, samp, span, ch, trig, s0, scale, X, nr, Q); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -188,6 +188,7 @@ int Encoder::prepare(const uint8_t* wav, size_t len, std::string* err) {
     const int SC = sample_count_;
     filtered_.resize(size_t(ch));
     for (auto& v : filtered_) v.resize(size_t(std::max(SC, 1)));  // no fill: the workers below write every sample
+    pcm_.resize(size_t(std::max(SC, 1)) * size_t(ch));
     const uint8_t* d = wav + 44;
     // per-sample work in parallel blocks; every sequential f64 sum below keeps
     // the reference's order (encoder.lpr:1374-1425)
@@ -198,11 +199,16 @@ int Encoder::prepare(const uint8_t* wav, size_t len, std::string* err) {
         for (int i = k * kBlk; i < i1; ++i)
             for (int c = 0; c < ch; ++c) {
                 const uint8_t* b = d + (size_t(i) * ch + c) * 2;
-                filtered_[c][i] = double(int16_t(uint16_t(b[0] | (b[1] << 8)))) / 32767.0;
+                const int16_t v = int16_t(uint16_t(b[0] | (b[1] << 8)));
+                pcm_[size_t(i) * ch + c] = v;
+                filtered_[c][i] = double(v) / 32767.0;
             }
         const int z1 = std::min(std::max(SC, 1), (k + 1) * kBlk);  // zero padding past the WAV end
         for (int i = std::max(sc, k * kBlk); i < z1; ++i)
-            for (int c = 0; c < ch; ++c) filtered_[c][i] = 0.0;
+            for (int c = 0; c < ch; ++c) {
+                pcm_[size_t(i) * ch + c] = 0;
+                filtered_[c][i] = 0.0;
+            }
     });
     const int frame_count = int(fpc::ceil_pos(double(SC) / (double(sample_rate_) * (o.frame_length / 1000.0))));
     // ChunksPerFrame search only changes anything with -br (encoder.lpr:1337-1351)

@@ -113,9 +113,11 @@ class Encoder {
    private:
     void frame_host_src(FrameState& f) const;  // chunk count + srcData (encoder.lpr:467-485)
     // device DSP for frames (first frame index b): atten_div, neg / rev on the
-    // host side, features left in the device slab *dX at (*xoff)[i]
+    // host side, features left in the device slab *dX at (*xoff)[i]; with dQ,
+    // also the KNNFit queries Single(srcData) (N*CS floats per frame, frames
+    // concatenated) in the device slab *dQ
     int device_dsp(int b, std::vector<FrameState>& frames, void* dX, std::vector<int64_t>* xoff, double* ms,
-                   std::string* err);
+                   std::string* err, void* dQ = nullptr);
     // reconstruction of frames [b, b + frames.size()) on the device (after KNNFit)
     int device_recon(int b, const std::vector<FrameState>& frames, ReconOut* ro, std::string* err);
     void frame_reduce_post(FrameState& f, bool reduced) const;
@@ -127,6 +129,7 @@ class Encoder {
     int sample_count_ = 0;
     int block_ = 1;
     std::vector<std::vector<double, NoInitAlloc<double>>> filtered_;  // [ch][sample] = s / 32767
+    std::vector<int16_t, NoInitAlloc<int16_t>> pcm_;                  // [sample][ch] SmallInt, zero padded (device upload)
     std::vector<int> fr_start_, fr_end_;
 };
 

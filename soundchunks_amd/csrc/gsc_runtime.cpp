@@ -36,7 +36,8 @@ extern "C" hipError_t gsc_launch_atten(int cs, gsc::DspFrame* frames, int nframe
                                        int ch, int obd, hipStream_t st);
 extern "C" hipError_t gsc_launch_features(int cs, const gsc::DspFrame* frames, int nframes, int max_n,
                                           const double* samp, int64_t span, int ch, const double* trig, double s0,
-                                          double scale, float* X, uint8_t* nr, hipStream_t st);
+                                          double scale, float* X, uint8_t* nr, float* Q, hipStream_t st);
+extern "C" hipError_t gsc_launch_pcm(const int16_t* pcm, int64_t span, int ch, double* samp, hipStream_t st);
 extern "C" hipError_t gsc_launch_knnfit(int CS, gsc::FitFrame* frames, int nframes, int max_n, int max_r,
                                         const float* cand, const float* q, int* out, hipStream_t st);
 extern "C" hipError_t gsc_launch_recon(const gsc::ReconFrame* frames, int nframes, int max_n, int cs, int ch, int bd,
@@ -286,6 +287,18 @@ int run_reduce_batch_dev(int D, int K, int precision, const std::vector<int>& Ns
     HIP_TRY(hipMemcpy(C->data(), dC.p, sizeof(float) * C->size(), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(clusters->data(), dI.p, sizeof(int) * size_t(no), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(fr.data(), dFr.p, sizeof(ReduceFrame) * size_t(nf), hipMemcpyDeviceToHost));
+    if (std::getenv("GSC_HOST_TIMING")) {  // spread of the frames' finishing times (the scan tail)
+        std::vector<uint64_t> t;
+        for (int i = 0; i < nf; ++i)
+            if (fr[i].t_done) t.push_back(fr[i].t_done);
+        if (!t.empty()) {
+            std::sort(t.begin(), t.end());
+            const double last = double(t.back());
+            auto at = [&](double q) { return (last - double(t[size_t(q * double(t.size() - 1))])) / 1e5; };
+            std::fprintf(stderr, "scan tail: frames finished [ms before the last] min %.1f p10 %.1f p50 %.1f p90 %.1f\n",
+                         at(0.0), at(0.1), at(0.5), at(0.9));
+        }
+    }
     iters->resize(size_t(nf));
     slow->resize(size_t(nf));
     for (int i = 0; i < nf; ++i) {
@@ -418,9 +431,10 @@ int run_knnfit_overflow(int CS, const std::vector<FitFrame>& fr, const std::vect
     return 0;
 }
 
+// q: host queries, or empty with qdev = the device query slab (same layout)
 int run_knnfit_batch(int CS, const std::vector<int>& Rs, const std::vector<int>& Ns, const std::vector<float>& eps,
                      const std::vector<float>& cand, const std::vector<float>& q, std::vector<int>* best,
-                     double* knn_ms) {
+                     double* knn_ms, const float* qdev = nullptr) {
     const int nf = int(Ns.size());
     if (nf == 0) return 0;
     std::vector<FitFrame> fr(static_cast<size_t>(nf));
@@ -443,17 +457,20 @@ int run_knnfit_batch(int CS, const std::vector<int>& Rs, const std::vector<int>&
     DevBuf<int> dOut;
     DevBuf<FitFrame> dFr;
     HIP_TRY(dCand.alloc(size_t(co)));
-    HIP_TRY(dQ.alloc(size_t(qo)));
+    if (!qdev) {
+        HIP_TRY(dQ.alloc(size_t(qo)));
+        HIP_TRY(hipMemcpy(dQ.p, q.data(), sizeof(float) * size_t(qo), hipMemcpyHostToDevice));
+        qdev = dQ.p;
+    }
     HIP_TRY(dOut.alloc(size_t(qo / CS)));
     HIP_TRY(dFr.alloc(size_t(nf)));
     HIP_TRY(hipMemcpy(dCand.p, cand.data(), sizeof(float) * size_t(co), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(dQ.p, q.data(), sizeof(float) * size_t(qo), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(dFr.p, fr.data(), sizeof(FitFrame) * size_t(nf), hipMemcpyHostToDevice));
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
     HIP_TRY(hipEventRecord(e0, nullptr));
-    HIP_TRY(gsc_launch_knnfit(CS, dFr.p, nf, maxN, maxR, dCand.p, dQ.p, dOut.p, nullptr));
+    HIP_TRY(gsc_launch_knnfit(CS, dFr.p, nf, maxN, maxR, dCand.p, qdev, dOut.p, nullptr));
     HIP_TRY(hipEventRecord(e1, nullptr));
     HIP_TRY(hipEventSynchronize(e1));
     float t = 0;
@@ -469,7 +486,12 @@ int run_knnfit_batch(int CS, const std::vector<int>& Rs, const std::vector<int>&
         if (fr[i].overflow > 0) ov_frames.push_back(i);
     if (!ov_frames.empty()) {
         const double t0 = now_ms();
-        if (run_knnfit_overflow(CS, fr, ov_frames, eps, cand, q, best) != 0) return -1;
+        std::vector<float> qh;
+        if (q.empty()) {  // the overflow replay reads host queries
+            qh.resize(size_t(qo));
+            HIP_TRY(hipMemcpy(qh.data(), qdev, sizeof(float) * size_t(qo), hipMemcpyDeviceToHost));
+        }
+        if (run_knnfit_overflow(CS, fr, ov_frames, eps, cand, q.empty() ? qh : q, best) != 0) return -1;
         if (knn_ms) *knn_ms += now_ms() - t0;
     }
     return 0;
@@ -480,7 +502,7 @@ int run_knnfit_batch(int CS, const std::vector<int>& Rs, const std::vector<int>&
 // ---- Encoder::device_dsp: FindAttenuationDivider + features on the device --
 // dXv: DevBuf<float>* that receives the feature slab (kept for the Reduce).
 int Encoder::device_dsp(int b, std::vector<FrameState>& frames, void* dXv, std::vector<int64_t>* xoff, double* ms,
-                        std::string* err) {
+                        std::string* err, void* dQv) {
     auto& dX = *static_cast<DevBuf<float>*>(dXv);
     const int cs = opt_.chunk_size, ch = channels_, nfr = int(frames.size());
     const int obd = (1 << (opt_.chunk_bit_depth - 1)) - 1;
@@ -509,26 +531,38 @@ int Encoder::device_dsp(int b, std::vector<FrameState>& frames, void* dXv, std::
     DevBuf<double> dS, dT;
     DevBuf<DspFrame> dF;
     DevBuf<uint8_t> dNR;
+    DevBuf<int16_t> dP;
+    float* dQ = nullptr;
     const double t0 = now_ms();
     if (dS.alloc(size_t(ch) * size_t(span)) != hipSuccess || dT.alloc(trig.size()) != hipSuccess ||
-        dF.alloc(size_t(nfr)) != hipSuccess || dNR.alloc(size_t(co)) != hipSuccess || dX.alloc(size_t(xo)) != hipSuccess) {
+        dF.alloc(size_t(nfr)) != hipSuccess || dNR.alloc(size_t(co)) != hipSuccess || dX.alloc(size_t(xo)) != hipSuccess ||
+        dP.alloc(size_t(ch) * size_t(span)) != hipSuccess) {
         *err = "device DSP: out of device memory";
         return -1;
+    }
+    if (dQv) {
+        auto& q = *static_cast<DevBuf<float>*>(dQv);
+        if (q.alloc(size_t(co) * size_t(cs)) != hipSuccess) {
+            *err = "device DSP: out of device memory";
+            return -1;
+        }
+        dQ = q.p;
     }
     auto chk = [&](hipError_t r, const char* what) {
         if (r == hipSuccess) return true;
         *err = std::string("device DSP: ") + what + ": " + hipGetErrorString(r);
         return false;
     };
-    for (int j = 0; j < ch; ++j)
-        if (!chk(hipMemcpy(dS.p + size_t(j) * size_t(span), filtered_[j].data() + s_first, sizeof(double) * size_t(span),
-                           hipMemcpyHostToDevice),
-                 "sample upload"))
-            return -1;
+    // the SmallInt samples of the span (a quarter of the f64 bytes), converted on the device
+    if (!chk(hipMemcpy(dP.p, pcm_.data() + size_t(s_first) * ch, sizeof(int16_t) * size_t(ch) * size_t(span),
+                       hipMemcpyHostToDevice),
+             "sample upload") ||
+        !chk(gsc_launch_pcm(dP.p, span, ch, dS.p, nullptr), "sample conversion"))
+        return -1;
     if (!chk(hipMemcpy(dT.p, trig.data(), sizeof(double) * trig.size(), hipMemcpyHostToDevice), "trig upload") ||
         !chk(hipMemcpy(dF.p, df.data(), sizeof(DspFrame) * size_t(nfr), hipMemcpyHostToDevice), "frame upload") ||
         !chk(gsc_launch_atten(cs, dF.p, nfr, dS.p, span, ch, obd, nullptr), "atten launch") ||
-        !chk(gsc_launch_features(cs, dF.p, nfr, max_n, dS.p, span, ch, dT.p, s0, scale, dX.p, dNR.p, nullptr),
+        !chk(gsc_launch_features(cs, dF.p, nfr, max_n, dS.p, span, ch, dT.p, s0, scale, dX.p, dNR.p, dQ, nullptr),
              "features launch"))
         return -1;
     std::vector<uint8_t> nr(static_cast<size_t>(co));
@@ -662,9 +696,9 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
         frame_host_src(f);
     });
     double dsp_ms = 0;
-    DevBuf<float> dFeat;
+    DevBuf<float> dFeat, dQry;
     std::vector<int64_t> feat_off;
-    if (nfr > 0 && device_dsp(b, frames, &dFeat, &feat_off, &dsp_ms, err) != 0) return -1;
+    if (nfr > 0 && device_dsp(b, frames, &dFeat, &feat_off, &dsp_ms, err, &dQry) != 0) return -1;
     double t1 = now_ms();
     // --- Reduce on the device for frames with more chunks than ChunksPerFrame
     std::vector<int> red_idx, Ns;
@@ -724,14 +758,14 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
     {
         std::vector<int> Rs(static_cast<size_t>(nfr)), Nq(static_cast<size_t>(nfr));
         std::vector<float> eps(static_cast<size_t>(nfr));
-        std::vector<size_t> coff(size_t(nfr) + 1, 0), qoff(size_t(nfr) + 1, 0);
+        std::vector<size_t> coff(size_t(nfr) + 1, 0);
         for (int i = 0; i < nfr; ++i) {
             Rs[i] = frames[i].r;
             Nq[i] = frames[i].n;
             coff[i + 1] = coff[i] + size_t(frames[i].r) * cs;
-            qoff[i + 1] = qoff[i] + frames[i].src.size();
         }
-        std::vector<float> cand(coff[nfr]), q(qoff[nfr]);
+        // the queries Single(srcData) are already in HBM (device DSP)
+        std::vector<float> cand(coff[nfr]), q;
         const int bd = opt_.chunk_bit_depth;
         const int obd = (1 << (bd - 1)) - 1;
         parallel_for(nfr, host_threads(), [&](int i) {
@@ -753,12 +787,10 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
                     *cp++ = float(v);
                 }
             }
-            float* qp = q.data() + qoff[i];
-            for (size_t k = 0; k < f.src.size(); ++k) qp[k] = float(f.src[k]);
         });
         std::vector<int> best;
         t2c = now_ms();
-        if (run_knnfit_batch(cs, Rs, Nq, eps, cand, q, &best, &knn_ms) != 0) {
+        if (run_knnfit_batch(cs, Rs, Nq, eps, cand, q, &best, &knn_ms, dQry.p) != 0) {
             *err = t_err;
             return -1;
         }
@@ -782,6 +814,14 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
                      "host timing [ms]: frames+dsp %.1f (dsp %.1f) | reduce (yakmo %.1f scan %.1f) %.1f | reduce_post %.1f |"
                      " knn_stage %.1f | knnfit call %.1f (kernel %.1f) | knn_post+save+concat %.1f\n",
                      t1 - t0, dsp_ms, yak_ms, scan_ms, t2 - t1, t2b - t2, t2c - t2b, t3 - t2c, knn_ms, t4 - t3);
+    if (std::getenv("GSC_HOST_TIMING") && !red_idx.empty()) {  // per-frame pass counts (scan tail)
+        std::vector<int> h(kMaxScanIters + 1, 0);
+        for (int i : red_idx) h[std::min(kMaxScanIters, std::max(0, frames[i].scan_iters))]++;
+        std::fprintf(stderr, "scan passes histogram:");
+        for (int v = 0; v <= kMaxScanIters; ++v)
+            if (h[v]) std::fprintf(stderr, " %d:%d", v, h[v]);
+        std::fprintf(stderr, "\n");
+    }
     if (tim) {
         tim->host_frames_ms = t1 - t0 - dsp_ms;
         tim->gpu_dsp_ms = dsp_ms;

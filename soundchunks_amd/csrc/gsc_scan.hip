@@ -1685,6 +1685,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         frp->restarts += restarts;
         frp->err = err;
         frp->done = done ? 1 : 0;
+        if (done) frp->t_done = __builtin_amdgcn_s_memrealtime();  // diagnostic: the scan tail
     }
     // the next pass's tree build and rate lookups read C and prev_cnt as
     // written above by other lanes (and, two-CU frames, by the partner)
