@@ -220,8 +220,12 @@ def main():
                      "hbm_gbs": None if traffic is None else round(traffic / avg_launch_s / 1e9, 2),
                      "hbm_frac": None if traffic is None else round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 6),
                      "avg_launch_ms": round(avg_launch_s * 1e3, 3), "ops_per_launch": ops / launches},
+        # host_post_ms: what the KNNFit / prune / packing pipeline adds after the
+        # scan; post_overlap_ms: the part of it that ran in the scan tail
         "stages_ms": {k: round(tm[k], 1) for k in ("host_prepare_ms", "host_frames_ms", "gpu_dsp_ms", "gpu_yakmo_ms",
-                                                    "gpu_scan_ms", "gpu_knnfit_ms", "host_post_ms", "total_ms")},
+                                                    "gpu_scan_ms", "gpu_knnfit_ms", "host_post_ms", "post_overlap_ms",
+                                                    "total_ms")},
+        "post_groups": tm["post_groups"],
         "scan": {"passes": tm["scan_passes"], "searches": tm["scan_point_passes"], "exact_dfs": tm["scan_slow"],
                  "solo_resolutions": tm["scan_restarts"]},
     }

@@ -145,6 +145,8 @@ typedef struct {
     int scan_launches, knnfit_launches;
     long long scan_restarts;     /* batched KNNScanReduce pipeline restarts */
     double gpu_dsp_ms;           /* device DSP incl. sample upload (attenuation divider, features) */
+    double post_overlap_ms;      /* KNNFit + prune/sort + packing run while other frames were still scanning */
+    int post_groups;             /* frame groups the post-processing pipeline ran */
 } gsc_timing;
 void gsc_last_timing(gsc_timing *t);
 

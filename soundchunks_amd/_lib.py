@@ -54,6 +54,8 @@ class GscTiming(ctypes.Structure):
         ("knnfit_launches", ctypes.c_int),
         ("scan_restarts", ctypes.c_longlong),
         ("gpu_dsp_ms", ctypes.c_double),
+        ("post_overlap_ms", ctypes.c_double),
+        ("post_groups", ctypes.c_int),
     ]
 
 

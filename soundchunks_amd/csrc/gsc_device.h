@@ -32,7 +32,13 @@ struct ReduceFrame {
     int32_t tree_exact;   // out: passes whose kd-tree needed the sequential build (median ties)
     int32_t xseq;         // two-CU frames (D = 32, K = 4096): tag of the last hand-off between the two CUs
     uint64_t t_done;      // out: s_memrealtime (100 MHz) when the batched kernel finished the frame
+    // optional (batched kernel): when the frame is done, its final clusters are
+    // copied to cl_host (host-mapped, N ints) and then *notify is set (system
+    // scope), so the host post-processes it while other frames still scan
+    int32_t* cl_host;
+    int32_t* notify;
     uint64_t stamps[128]; // out (GSC_STAMPS builds only): per-phase cycles, 16 per wave
+    uint64_t ystamps[16]; // out (GSC_STAMPS builds only): yakmo phase cycles (gsc_yakmo.hip)
 };
 
 // One frame of the encoder's per-frame DSP: FindAttenuationDivider
@@ -65,6 +71,20 @@ struct FitFrame {
     float eps;
     int32_t overflow;     // out: queries whose tie set exceeds ANN's 64-NN bucket
 };
+
+// One frame of the KNNFit post-processing and SaveStream's index bitstream
+// (gsc_pack.hip; encoder.lpr:966-977, 1044-1106).
+struct PackFrame {
+    int64_t out_off;      // N ints: KNNFit best (4c + 2neg + rev) at best + out_off
+    int64_t r_off;        // R ints: use counts (out) / old -> new index map (in) at + r_off
+    int64_t w_off;        // bitstream: pack_word_capacity(N) zeroed u32 words at words + w_off
+    int32_t N, R;         // chunkRefs count, reducedChunks count before pruning (<= kMaxK)
+    int32_t nbits;        // out: bits of the stream (16-bit words written = ceil(nbits / 16))
+    int32_t pad_;
+};
+
+// u32 words that hold the index stream of n chunks (<= 17 bits per code)
+inline int64_t pack_word_capacity(int64_t n) { return (n * 17 + 31) / 32 + 1; }
 
 // ANN kd-tree (ANN_KD_STD, bs = 1) over n points, heap-indexed split nodes
 // (gsc_ann.hip): the drop-in ABI's trees and the KNNFit candidate trees.

@@ -130,12 +130,6 @@ void fpc_quicksort(int* items, const int* count, int L, int R) {
     } while (I < R);
 }
 
-inline int bsr_word(unsigned v) {
-    int r = 0;
-    while (v >>= 1) ++r;
-    return r;
-}
-
 }  // namespace
 
 void warm_trig_tables(int cs) { (void)trig_for(cs); }
@@ -346,23 +340,20 @@ void Encoder::frame_reduce_post(FrameState& f, bool reduced) const {
     }
 }
 
-// KNNFit post: flags, prune unused, FPC QuickSort by use count, reindex (encoder.lpr:960-977)
-void Encoder::frame_knnfit_post(FrameState& f) const {
+// KNNFit post on the host (encoder.lpr:966-977): drop the entries no chunk
+// uses, FPC QuickSort the survivors by use count, and reorder dstData and
+// the attenuations.  remap[old] = new index (-1 for a dropped entry).  The
+// per-chunk part (final index, dstNegative, dstReversed) and the index
+// bitstream run on the device (gsc_pack.hip).
+void Encoder::frame_prune(FrameState& f, const int* use, int* remap) const {
     const int cs = opt_.chunk_size;
     f.r_before_prune = f.r;
-    std::vector<int> use(size_t(f.r), 0);
-    f.red.assign(size_t(f.n), 0);
-    for (int i = 0; i < f.n; ++i) {
-        const int b = f.best[i];
-        f.neg[i] = (b & 2) != 0;
-        f.rev[i] = (b & 1) != 0;
-        f.red[i] = b >> 2;
-        ++use[b >> 2];
-    }
     std::vector<int> alive;
     alive.reserve(size_t(f.r));
-    for (int i = 0; i < f.r; ++i)
+    for (int i = 0; i < f.r; ++i) {
+        remap[i] = -1;
         if (use[i] != 0) alive.push_back(i);
+    }
     const int na = int(alive.size());
     std::vector<int> cnt(static_cast<size_t>(std::max(na, 1))), order(static_cast<size_t>(std::max(na, 1)));
     for (int i = 0; i < na; ++i) {
@@ -370,7 +361,6 @@ void Encoder::frame_knnfit_post(FrameState& f) const {
         order[i] = i;
     }
     if (na > 1) fpc_quicksort(order.data(), cnt.data(), 0, na - 1);
-    std::vector<int> remap(size_t(f.r), -1);
     std::vector<int16_t> ndst(size_t(std::max(na, 1)) * cs);
     std::vector<uint8_t> natt(static_cast<size_t>(std::max(na, 1)));
     for (int i = 0; i < na; ++i) {
@@ -379,14 +369,15 @@ void Encoder::frame_knnfit_post(FrameState& f) const {
         std::memcpy(&ndst[size_t(i) * cs], &f.rdst[size_t(o) * cs], sizeof(int16_t) * cs);
         natt[i] = f.ratten[o];
     }
-    for (int i = 0; i < f.n; ++i) f.red[i] = remap[f.red[i]];
     f.rdst.swap(ndst);
     f.ratten.swap(natt);
     f.r = na;
 }
 
-// TFrame.SaveStream (encoder.lpr:980-1107)
-void Encoder::frame_save(FrameState& f) const {
+// TFrame.SaveStream (encoder.lpr:980-1048) up to the band's chunk count:
+// header, attenuations, dstData.  The index stream that follows
+// (encoder.lpr:1050-1106) comes from the device packer.
+void Encoder::frame_save_head(FrameState& f) const {
     const int cs = opt_.chunk_size, bd = opt_.chunk_bit_depth, ch = channels_;
     std::vector<uint8_t>& o = f.stream;
     o.clear();
@@ -424,36 +415,6 @@ void Encoder::frame_save(FrameState& f) const {
         }
     }
     w32(uint32_t(f.n / ch));
-    int bit_cnt = 0;
-    uint32_t bits = 0;
-    int prev_vc = -1;
-    for (int j = 0; j < f.n; ++j) {
-        const int idx = f.red[j];
-        const int vc = idx == 0 ? 0 : bsr_word(unsigned(idx)) / 3;
-        uint64_t code = uint64_t(f.neg[j] ? 1 : 0) | (uint64_t(f.rev[j] ? 1 : 0) << 1);
-        int size = 2;
-        if (vc == prev_vc) {
-            size += 1;
-        } else {
-            code |= uint64_t(1) << size;
-            size += 1;
-            code |= uint64_t(vc) << size;
-            size += 2;
-        }
-        for (int k = vc; k >= 0; --k) {
-            code |= uint64_t((idx >> (k * 3)) & 7) << size;
-            size += 3;
-        }
-        bits = uint32_t(bits | (uint32_t(code) << bit_cnt));
-        bit_cnt += size;
-        if (bit_cnt >= 16) {
-            bit_cnt -= 16;
-            w16(bits & 0xffff);
-            bits >>= 16;
-        }
-        prev_vc = vc;
-    }
-    if (bit_cnt > 0) w16(bits & 0xffff);
 }
 
 }  // namespace gsc

@@ -85,6 +85,9 @@ struct ReconOut {
     double ms = 0;
 };
 
+// device slabs + stream of the KNNFit/packing pipeline of one encode (gsc_runtime.cpp)
+struct PostCtx;
+
 // -py reducer (gsc_birch_host.cpp): cluster.py's Birch labels of N samples
 int birch_reduce_labels(int n, int d, const float* feat, int K, int* labels, std::string* err);
 
@@ -121,8 +124,13 @@ class Encoder {
     // reconstruction of frames [b, b + frames.size()) on the device (after KNNFit)
     int device_recon(int b, const std::vector<FrameState>& frames, ReconOut* ro, std::string* err);
     void frame_reduce_post(FrameState& f, bool reduced) const;
-    void frame_knnfit_post(FrameState& f) const;
-    void frame_save(FrameState& f) const;
+    // KNNFit prune + sort by use count (use[r] in, remap[r] out)
+    void frame_prune(FrameState& f, const int* use, int* remap) const;
+    // SaveStream's header, attenuations and dstData (the index stream is packed on the device)
+    void frame_save_head(FrameState& f) const;
+    // KNNFit, prune/sort and index packing of frames ids (gsc_runtime.cpp)
+    int post_group(std::vector<FrameState>& frames, const std::vector<int>& ids, const std::vector<char>& reduced,
+                   PostCtx& ctx, std::string* err);
 
     gsc_options opt_;
     int channels_ = 0, sample_rate_ = 0;

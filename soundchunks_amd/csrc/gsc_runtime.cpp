@@ -15,6 +15,7 @@
 #include <new>
 #include <string>
 #include <strings.h>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -45,6 +46,10 @@ extern "C" hipError_t gsc_launch_recon(const gsc::ReconFrame* frames, int nframe
                                        hipStream_t st);
 extern "C" hipError_t gsc_launch_sqdiff(const int16_t* a, const int16_t* b, int64_t n, unsigned long long* acc,
                                         hipStream_t st);
+extern "C" hipError_t gsc_launch_usecount(const gsc::PackFrame* frames, int nframes, const int* best, int* counts,
+                                          hipStream_t st);
+extern "C" hipError_t gsc_launch_pack(gsc::PackFrame* frames, int nframes, const int* best, const int* remap,
+                                      uint32_t* words, uint32_t* codes, hipStream_t st);
 extern "C" hipError_t gsc_launch_ann_build_many(const void* trees, int ntrees, hipStream_t st);
 extern "C" hipError_t gsc_launch_knnfit_ann(const void* trees, const void* jobs, int njobs, const float* q, int* out,
                                             float* pq_key, void* pq_node, int pq_cap, hipStream_t st);
@@ -225,9 +230,13 @@ std::vector<float> rate_table(int n) {
 // Reduce (yakmo seeding + KNNScanReduce) for a batch of frames; X/C host arrays
 // are concatenated per frame (N_f*D and K*D floats).
 // X: device slab, frame i's N_i x D features at dX + xoff[i]
+// cl_host / notify (optional, device pointers of host-mapped memory): the
+// batched kernel copies a frame's final clusters to cl_host + its n_off and
+// then sets notify[i], so the host can post-process it during the scan tail
 int run_reduce_batch_dev(int D, int K, int precision, const std::vector<int>& Ns, const std::vector<int64_t>& xoff,
                          const float* dX, std::vector<float>* C, std::vector<int>* clusters, std::vector<int>* iters,
-                         std::vector<int>* slow, long long* restarts, double* yakmo_ms, double* scan_ms) {
+                         std::vector<int>* slow, long long* restarts, double* yakmo_ms, double* scan_ms,
+                         int* cl_host = nullptr, int* notify = nullptr) {
     // launches: one yakmo launch + kMaxScanIters scan launches per batch
     const int nf = int(Ns.size());
     if (nf == 0) return 0;
@@ -250,6 +259,10 @@ int run_reduce_batch_dev(int D, int K, int precision, const std::vector<int>& Ns
     for (int i = 0; i < nf; ++i) {
         fr[i].k_off = no + int64_t(i) * K;
         fr[i].ka_off = no + int64_t(nf + i) * K;
+        if (cl_host && notify) {
+            fr[i].cl_host = cl_host + fr[i].n_off;
+            fr[i].notify = notify + i;
+        }
     }
     DevBuf<float> dC, dF, dRate;
     DevBuf<int> dI;
@@ -298,6 +311,16 @@ int run_reduce_batch_dev(int D, int K, int precision, const std::vector<int>& Ns
             std::fprintf(stderr, "scan tail: frames finished [ms before the last] min %.1f p10 %.1f p50 %.1f p90 %.1f\n",
                          at(0.0), at(0.1), at(0.5), at(0.9));
         }
+    }
+    if (std::getenv("GSC_HOST_TIMING") && nf > 0 && fr[0].ystamps[6] + fr[0].ystamps[1] + fr[0].ystamps[2] != 0) {
+        // stamps builds: yakmo phase clocks, mean over frames (cycles per pick)
+        double m[16] = {};
+        for (int i = 0; i < nf; ++i)
+            for (int k = 0; k < 16; ++k) m[k] += double(fr[i].ystamps[k]) / double(nf) / double(K);
+        std::fprintf(stderr,
+                     "yakmo stamps [clk/pick]: chain pick %.0f fast %.0f slow %.0f wait %.0f (fast steps %.1f slow %.1f)"
+                     " | dist pick+sdlo %.0f compute %.0f wait %.0f\n",
+                     m[0], m[1], m[2], m[3], m[4], m[5], m[8], m[9], m[10]);
     }
     iters->resize(size_t(nf));
     slow->resize(size_t(nf));
@@ -497,7 +520,71 @@ int run_knnfit_batch(int CS, const std::vector<int>& Rs, const std::vector<int>&
     return 0;
 }
 
+// Pinned host staging, kept across encode calls (pinning ~100 MB per call
+// would cost more than the transfers).  Leaked on purpose: it lives until the
+// process exits, after the HIP runtime may already be gone.
+struct PinnedBuf {
+    unsigned flags = hipHostMallocDefault;
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
+        const hipError_t e = hipHostMalloc(&p, want, flags);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    template <typename T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+};
+
+struct PinnedArena {
+    std::mutex m;
+    // host-side DMA staging: candidates up, use counts down, remap up, words down, codes down
+    PinnedBuf cand, cnt, remap, words, codes;
+    // written by the scan kernel (fine-grained, mapped): final clusters and done flags
+    PinnedBuf cl{hipHostMallocMapped | hipHostMallocCoherent}, notify{hipHostMallocMapped | hipHostMallocCoherent};
+};
+
+PinnedArena& pinned_arena() {
+    static PinnedArena* a = new PinnedArena;
+    return *a;
+}
+
 }  // namespace
+
+// KNNFit + prune/sort + index packing of one encode, run on frame groups as
+// they become ready (frames that skip the Reduce at once, reduced frames when
+// the scan kernel signals them), on its own non-blocking stream so that the
+// groups run on the CUs that finished frames leave idle.
+struct PostCtx {
+    hipStream_t st = nullptr;
+    bool recon = false;
+    std::vector<int64_t> coff, roff, woff, noff;  // per frame: candidates (floats), R slots, words, chunks
+    DevBuf<float> dCand;
+    DevBuf<int> dBest, dCnt, dRemap;
+    DevBuf<uint32_t> dWords, dCodes;
+    DevBuf<FitFrame> dFit;
+    DevBuf<PackFrame> dPack;
+    const float* dQry = nullptr;
+    float* hCand = nullptr;
+    int *hCnt = nullptr, *hRemap = nullptr;
+    uint32_t *hWords = nullptr, *hCodes = nullptr;
+    int slot = 0;  // next descriptor slot in dFit / dPack
+    double knn_ms = 0;
+    int groups = 0;
+    ~PostCtx() {
+        if (st) {
+            (void)hipStreamSynchronize(st);
+            (void)hipStreamDestroy(st);
+        }
+    }
+};
 
 // ---- Encoder::device_dsp: FindAttenuationDivider + features on the device --
 // dXv: DevBuf<float>* that receives the feature slab (kept for the Reduce).
@@ -649,6 +736,200 @@ int Encoder::device_recon(int b, const std::vector<FrameState>& frames, ReconOut
     return 0;
 }
 
+int Encoder::post_group(std::vector<FrameState>& frames, const std::vector<int>& ids,
+                        const std::vector<char>& reduced, PostCtx& c, std::string* err) {
+    const int cs = opt_.chunk_size, bd = opt_.chunk_bit_depth, obd = (1 << (bd - 1)) - 1;
+    const int g = int(ids.size());
+    if (g == 0) return 0;
+    auto chk = [&](hipError_t r, const char* what) {
+        if (r == hipSuccess) return true;
+        *err = std::string("KNNFit/pack pipeline: ") + what + ": " + hipGetErrorString(r);
+        return false;
+    };
+    std::vector<float> eps(static_cast<size_t>(g));
+    // TFrame.Reduce's tail (cluster means, sort, reduced chunks) and the
+    // KNNFit candidates (encoder.lpr:843-889, 928-938), per frame on the host pool
+    parallel_for(g, host_threads(), [&](int k) {
+        FrameState& f = frames[size_t(ids[k])];
+        frame_reduce_post(f, reduced[size_t(ids[k])] != 0);
+        const double law = 1.0 / double(f.atten_div);
+        // epsilon (encoder.lpr:940-943), accumulated in Single
+        float acc = 1.0f;
+        for (int j = 0; j <= 15; ++j) acc = float(double(acc) + double(j) * law);
+        const float e1 = 1.0f / (float(1 << bd) * acc);
+        const float e2 = float(1.0 / 32767.0);
+        eps[size_t(k)] = e1 > e2 ? e1 : e2;
+        float* cp = c.hCand + c.coff[size_t(ids[k])];
+        for (int r = 0; r < f.r; ++r) {
+            double coeff = 1.0;
+            for (int a = 0; a <= f.ratten[r]; ++a) coeff += double(a) * law;
+            for (int j = 0; j < cs; ++j) {
+                double v = double(f.rdst[size_t(r) * cs + j]) / (double(obd) * coeff);
+                v = std::min(1.0, std::max(-1.0, v));
+                *cp++ = float(v);
+            }
+        }
+    });
+    const int gb = c.slot;
+    c.slot += g;
+    std::vector<FitFrame> fit(static_cast<size_t>(g));
+    std::vector<PackFrame> pk(static_cast<size_t>(g));
+    int maxN = 0, maxR = 0;
+    for (int k = 0; k < g; ++k) {
+        const size_t i = size_t(ids[k]);
+        const FrameState& f = frames[i];
+        if (f.r > kMaxK) {
+            *err = "KNNFit: more than 4096 reduced chunks in a frame";
+            return -1;
+        }
+        fit[size_t(k)] = FitFrame{c.coff[i], c.noff[i] * cs, c.noff[i], f.r, f.n, eps[size_t(k)], 0};
+        pk[size_t(k)] = PackFrame{c.noff[i], c.roff[i], c.woff[i], f.n, f.r, 0, 0};
+        maxN = std::max(maxN, f.n);
+        maxR = std::max(maxR, f.r);
+    }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (!chk(hipEventCreate(&e0), "event") || !chk(hipEventCreate(&e1), "event")) return -1;
+    struct EvGuard {
+        hipEvent_t a, b;
+        ~EvGuard() {
+            (void)hipEventDestroy(a);
+            (void)hipEventDestroy(b);
+        }
+    } evg{e0, e1};
+    const hipStream_t st = c.st;
+    bool ok = chk(hipMemcpyAsync(c.dFit.p + gb, fit.data(), sizeof(FitFrame) * size_t(g), hipMemcpyHostToDevice, st),
+                  "upload") &&
+              chk(hipMemcpyAsync(c.dPack.p + gb, pk.data(), sizeof(PackFrame) * size_t(g), hipMemcpyHostToDevice, st),
+                  "upload");
+    for (int k = 0; ok && k < g; ++k) {
+        const size_t i = size_t(ids[k]);
+        ok = chk(hipMemcpyAsync(c.dCand.p + c.coff[i], c.hCand + c.coff[i], sizeof(float) * size_t(frames[i].r) * cs,
+                                hipMemcpyHostToDevice, st),
+                 "candidate upload");
+    }
+    ok = ok && chk(hipEventRecord(e0, st), "event") &&
+         chk(gsc_launch_knnfit(cs, c.dFit.p + gb, g, maxN, maxR, c.dCand.p, c.dQry, c.dBest.p, st), "KNNFit launch") &&
+         chk(hipEventRecord(e1, st), "event") &&
+         chk(gsc_launch_usecount(c.dPack.p + gb, g, c.dBest.p, c.dCnt.p, st), "use count launch") &&
+         chk(hipMemcpyAsync(fit.data(), c.dFit.p + gb, sizeof(FitFrame) * size_t(g), hipMemcpyDeviceToHost, st),
+             "download");
+    for (int k = 0; ok && k < g; ++k) {
+        const size_t i = size_t(ids[k]);
+        ok = chk(hipMemcpyAsync(c.hCnt + c.roff[i], c.dCnt.p + c.roff[i], sizeof(int) * size_t(frames[i].r),
+                                hipMemcpyDeviceToHost, st),
+                 "use count download");
+    }
+    if (!ok || !chk(hipStreamSynchronize(st), "KNNFit")) return -1;
+    float t = 0;
+    if (hipEventElapsedTime(&t, e0, e1) == hipSuccess) c.knn_ms += t;
+    // queries whose tie set exceeds ANN's 64-NN bucket: ANN's priority search
+    // over the frame's candidate tree (rare; it waits for the scan)
+    std::vector<int> ovk;
+    for (int k = 0; k < g; ++k)
+        if (fit[size_t(k)].overflow > 0) ovk.push_back(k);
+    if (!ovk.empty()) {
+        const double t0 = now_ms();
+        std::vector<FitFrame> lf;
+        std::vector<float> lcand, lq, leps;
+        std::vector<int> lbest, lidx;
+        for (int k : ovk) {
+            const FrameState& f = frames[size_t(ids[k])];
+            FitFrame x = fit[size_t(k)];
+            x.cand_off = int64_t(lcand.size());
+            x.q_off = int64_t(lq.size());
+            x.out_off = int64_t(lbest.size());
+            lcand.insert(lcand.end(), c.hCand + fit[size_t(k)].cand_off,
+                         c.hCand + fit[size_t(k)].cand_off + size_t(f.r) * cs);
+            lq.resize(lq.size() + size_t(f.n) * cs);
+            lbest.resize(lbest.size() + size_t(f.n));
+            if (!chk(hipMemcpyAsync(lq.data() + x.q_off, c.dQry + fit[size_t(k)].q_off, sizeof(float) * size_t(f.n) * cs,
+                                    hipMemcpyDeviceToHost, st),
+                     "query download") ||
+                !chk(hipMemcpyAsync(lbest.data() + x.out_off, c.dBest.p + fit[size_t(k)].out_off,
+                                    sizeof(int) * size_t(f.n), hipMemcpyDeviceToHost, st),
+                     "download"))
+                return -1;
+            lidx.push_back(int(lf.size()));
+            leps.push_back(x.eps);
+            lf.push_back(x);
+        }
+        if (!chk(hipStreamSynchronize(st), "download")) return -1;
+        if (run_knnfit_overflow(cs, lf, lidx, leps, lcand, lq, &lbest) != 0) {
+            *err = t_err;
+            return -1;
+        }
+        for (size_t j = 0; j < ovk.size(); ++j)
+            if (!chk(hipMemcpyAsync(c.dBest.p + fit[size_t(ovk[j])].out_off, lbest.data() + lf[j].out_off,
+                                    sizeof(int) * size_t(lf[j].N), hipMemcpyHostToDevice, st),
+                     "upload"))
+                return -1;
+        ok = chk(gsc_launch_usecount(c.dPack.p + gb, g, c.dBest.p, c.dCnt.p, st), "use count launch");
+        for (int k = 0; ok && k < g; ++k) {
+            const size_t i = size_t(ids[k]);
+            ok = chk(hipMemcpyAsync(c.hCnt + c.roff[i], c.dCnt.p + c.roff[i], sizeof(int) * size_t(frames[i].r),
+                                    hipMemcpyDeviceToHost, st),
+                     "use count download");
+        }
+        if (!ok || !chk(hipStreamSynchronize(st), "use counts")) return -1;
+        c.knn_ms += now_ms() - t0;
+    }
+    // prune + sort by use count on the host, then the index stream on the device
+    parallel_for(g, host_threads(), [&](int k) {
+        const size_t i = size_t(ids[k]);
+        frame_prune(frames[i], c.hCnt + c.roff[i], c.hRemap + c.roff[i]);
+    });
+    ok = true;
+    for (int k = 0; ok && k < g; ++k) {
+        const size_t i = size_t(ids[k]);
+        ok = chk(hipMemcpyAsync(c.dRemap.p + c.roff[i], c.hRemap + c.roff[i],
+                                sizeof(int) * size_t(frames[i].r_before_prune), hipMemcpyHostToDevice, st),
+                 "remap upload");
+    }
+    ok = ok && chk(gsc_launch_pack(c.dPack.p + gb, g, c.dBest.p, c.dRemap.p, c.dWords.p, c.recon ? c.dCodes.p : nullptr,
+                                   st),
+                   "pack launch") &&
+         chk(hipMemcpyAsync(pk.data(), c.dPack.p + gb, sizeof(PackFrame) * size_t(g), hipMemcpyDeviceToHost, st),
+             "download") &&
+         chk(hipStreamSynchronize(st), "pack");
+    for (int k = 0; ok && k < g; ++k) {
+        const size_t i = size_t(ids[k]);
+        const int64_t nw = (int64_t(pk[size_t(k)].nbits) + 31) / 32;  // whole u32 words (>= the 16-bit words used)
+        if (nw > pack_word_capacity(frames[i].n)) {
+            *err = "index packer overran its word slab";
+            return -1;
+        }
+        ok = chk(hipMemcpyAsync(c.hWords + c.woff[i], c.dWords.p + c.woff[i], sizeof(uint32_t) * size_t(nw),
+                                hipMemcpyDeviceToHost, st),
+                 "stream download");
+        if (ok && c.recon)
+            ok = chk(hipMemcpyAsync(c.hCodes + c.noff[i], c.dCodes.p + c.noff[i], sizeof(uint32_t) * size_t(frames[i].n),
+                                    hipMemcpyDeviceToHost, st),
+                     "code download");
+    }
+    if (!ok || !chk(hipStreamSynchronize(st), "stream download")) return -1;
+    parallel_for(g, host_threads(), [&](int k) {
+        const size_t i = size_t(ids[k]);
+        FrameState& f = frames[i];
+        frame_save_head(f);
+        const size_t nbytes = size_t((pk[size_t(k)].nbits + 15) / 16) * 2;  // 16-bit words, the last zero-padded
+        const uint8_t* wb = reinterpret_cast<const uint8_t*>(c.hWords + c.woff[i]);
+        f.stream.insert(f.stream.end(), wb, wb + nbytes);
+        if (c.recon) {  // final index / dstNegative / dstReversed per chunk (reconstruction)
+            f.red.resize(size_t(f.n));
+            f.neg.resize(size_t(f.n));
+            f.rev.resize(size_t(f.n));
+            const uint32_t* cw = c.hCodes + c.noff[i];
+            for (int j = 0; j < f.n; ++j) {
+                f.red[size_t(j)] = int(cw[j] >> 2);
+                f.neg[size_t(j)] = uint8_t((cw[j] >> 1) & 1);
+                f.rev[size_t(j)] = uint8_t(cw[j] & 1);
+            }
+        }
+    });
+    c.groups += 1;
+    return 0;
+}
+
 int Encoder::dsp_frame(int fi, int* atten_div, std::vector<float>* feat, std::string* err) {
     if (ensure_device() != 0) {
         *err = t_err;
@@ -703,15 +984,122 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
     // --- Reduce on the device for frames with more chunks than ChunksPerFrame
     std::vector<int> red_idx, Ns;
     std::vector<int64_t> red_xoff;
+    std::vector<char> is_red(size_t(nfr), 0);
     for (int i = 0; i < nfr; ++i)
         if (opt_.precision > 0 && frames[i].n > K) {
             red_idx.push_back(i);
             Ns.push_back(frames[i].n);
             red_xoff.push_back(feat_off[i]);
+            is_red[size_t(i)] = 1;
         }
-    double yak_ms = 0, scan_ms = 0, knn_ms = 0;
+    const int nred = int(red_idx.size());
+    double yak_ms = 0, scan_ms = 0;
     long long passes = 0, slow = 0, restarts = 0;
-    if (!red_idx.empty() && opt_.python_reduce) {
+    // --- the KNNFit / prune / packing pipeline's slabs (whole range, allocated
+    // before the scan starts: nothing is allocated or freed while it runs)
+    PostCtx pc;
+    pc.recon = recon != nullptr;
+    pc.dQry = dQry.p;
+    pc.coff.resize(size_t(nfr));
+    pc.roff.resize(size_t(nfr));
+    pc.woff.resize(size_t(nfr));
+    pc.noff.resize(size_t(nfr));
+    int64_t nc = 0, nr = 0, nw = 0, nn = 0;
+    for (int i = 0; i < nfr; ++i) {
+        const int rmax = is_red[size_t(i)] ? K : frames[i].n;  // reducedChunks.Count before pruning
+        pc.coff[size_t(i)] = nc;
+        pc.roff[size_t(i)] = nr;
+        pc.woff[size_t(i)] = nw;
+        pc.noff[size_t(i)] = nn;
+        nc += int64_t(rmax) * cs;
+        nr += rmax;
+        nw += pack_word_capacity(frames[i].n);
+        nn += frames[i].n;
+    }
+    PinnedArena& pa = pinned_arena();
+    std::lock_guard<std::mutex> arena_lock(pa.m);
+    int64_t nred_pts = 0;
+    for (int n : Ns) nred_pts += n;
+    {
+        auto chk = [&](hipError_t r, const char* what) {
+            if (r == hipSuccess) return true;
+            *err = std::string("KNNFit/pack pipeline setup: ") + what + ": " + hipGetErrorString(r);
+            return false;
+        };
+        if (!chk(hipStreamCreateWithFlags(&pc.st, hipStreamNonBlocking), "stream") ||
+            !chk(pc.dCand.alloc(size_t(nc)), "alloc") || !chk(pc.dBest.alloc(size_t(nn)), "alloc") ||
+            !chk(pc.dCnt.alloc(size_t(nr)), "alloc") || !chk(pc.dRemap.alloc(size_t(nr)), "alloc") ||
+            !chk(pc.dWords.alloc(size_t(nw)), "alloc") || !chk(pc.dFit.alloc(size_t(std::max(nfr, 1))), "alloc") ||
+            !chk(pc.dPack.alloc(size_t(std::max(nfr, 1))), "alloc") ||
+            (pc.recon && !chk(pc.dCodes.alloc(size_t(nn)), "alloc")) ||
+            !chk(pa.cand.reserve(sizeof(float) * size_t(nc)), "pinned alloc") ||
+            !chk(pa.cnt.reserve(sizeof(int) * size_t(nr)), "pinned alloc") ||
+            !chk(pa.remap.reserve(sizeof(int) * size_t(nr)), "pinned alloc") ||
+            !chk(pa.words.reserve(sizeof(uint32_t) * size_t(nw)), "pinned alloc") ||
+            (pc.recon && !chk(pa.codes.reserve(sizeof(uint32_t) * size_t(nn)), "pinned alloc")) ||
+            !chk(pa.cl.reserve(sizeof(int) * size_t(std::max<int64_t>(nred_pts, 1))), "pinned alloc") ||
+            !chk(pa.notify.reserve(sizeof(int) * size_t(std::max(nred, 1))), "pinned alloc") ||
+            !chk(hipMemsetAsync(pc.dWords.p, 0, sizeof(uint32_t) * size_t(nw), pc.st), "memset"))
+            return -1;
+    }
+    pc.hCand = pa.cand.as<float>();
+    pc.hCnt = pa.cnt.as<int>();
+    pc.hRemap = pa.remap.as<int>();
+    pc.hWords = pa.words.as<uint32_t>();
+    pc.hCodes = pa.codes.as<uint32_t>();
+    int* notify = pa.notify.as<int>();
+    int* cl_host = pa.cl.as<int>();
+    std::memset(notify, 0, sizeof(int) * size_t(std::max(nred, 1)));
+    std::vector<int64_t> red_noff(size_t(nred) + 1, 0);  // reduced frame j's clusters at cl_host + red_noff[j]
+    std::vector<int> red_pos(size_t(nfr), -1);
+    for (int j = 0; j < nred; ++j) {
+        red_noff[size_t(j) + 1] = red_noff[size_t(j)] + Ns[size_t(j)];
+        red_pos[size_t(red_idx[size_t(j)])] = j;
+    }
+    // 0: scanning; 1: every frame's clusters are final (notified ones in
+    // cl_host, the others in cl_final); -1: the Reduce failed
+    std::atomic<int> scan_state{0};
+    std::vector<int> cl_final;
+    std::string post_err;
+    double t_scan_end = 0, overlap_ms = 0;
+    const bool batched_scan = nred > 0 && !opt_.python_reduce;
+    auto post_loop = [&]() -> int {
+        std::vector<char> done(size_t(nfr), 0);
+        int remaining = nfr;
+        while (remaining > 0) {
+            const int st = scan_state.load(std::memory_order_acquire);
+            if (st < 0) return 0;
+            std::vector<int> ids;
+            for (int i = 0; i < nfr; ++i) {
+                if (done[size_t(i)]) continue;
+                const int j = red_pos[size_t(i)];
+                const bool notified = j >= 0 && batched_scan && __atomic_load_n(&notify[j], __ATOMIC_ACQUIRE) != 0;
+                if (j < 0 || notified || st == 1) ids.push_back(i);
+            }
+            // during the scan, wait for a group worth a launch
+            if (ids.empty() || (st == 0 && int(ids.size()) < std::min(remaining, 8))) {
+                std::this_thread::sleep_for(std::chrono::microseconds(500));
+                continue;
+            }
+            for (int i : ids) {
+                const int j = red_pos[size_t(i)];
+                if (j < 0 || !batched_scan) continue;
+                FrameState& f = frames[size_t(i)];
+                if (__atomic_load_n(&notify[j], __ATOMIC_ACQUIRE) != 0)
+                    f.clusters.assign(cl_host + red_noff[size_t(j)], cl_host + red_noff[size_t(j) + 1]);
+                else
+                    f.clusters.assign(cl_final.begin() + long(red_noff[size_t(j)]),
+                                      cl_final.begin() + long(red_noff[size_t(j) + 1]));
+            }
+            const double tg = now_ms();
+            if (post_group(frames, ids, is_red, pc, &post_err) != 0) return -1;
+            if (st == 0) overlap_ms += now_ms() - tg;
+            for (int i : ids) done[size_t(i)] = 1;
+            remaining -= int(ids.size());
+        }
+        return 0;
+    };
+    if (nred > 0 && opt_.python_reduce) {
         // -py: TFrame.Reduce with PythonReduce (encoder.lpr:837-841): Birch labels
         // (gsc_birch_host.cpp), no yakmo and no KNNScanReduce
         const double tb = now_ms();
@@ -729,91 +1117,64 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
             f.scan_slow = 0;
         }
         scan_ms += now_ms() - tb;
-    } else if (!red_idx.empty()) {
-        std::vector<float> C;
-        std::vector<int> cl, it, sl;
-        g_scan_rounds.store(0);
-        if (run_reduce_batch_dev(D, K, opt_.precision, Ns, red_xoff, dFeat.p, &C, &cl, &it, &sl, &restarts, &yak_ms,
-                                 &scan_ms) != 0) {
-            *err = t_err;
-            return -1;
-        }
-        size_t no = 0;
-        for (size_t j = 0; j < red_idx.size(); ++j) {
-            FrameState& f = frames[red_idx[j]];
-            f.clusters.assign(cl.begin() + long(no), cl.begin() + long(no + size_t(f.n)));
-            no += size_t(f.n);
-            f.scan_iters = it[j];
-            f.scan_slow = sl[j];
-            passes += it[j];
-            slow += sl[j];
-        }
     }
-    double t2 = now_ms(), t2c = 0;
-    std::vector<char> is_red(size_t(nfr), 0);
-    for (int i : red_idx) is_red[i] = 1;
-    parallel_for(nfr, host_threads(), [&](int i) { frame_reduce_post(frames[i], is_red[i] != 0); });
-    const double t2b = now_ms();
-    // --- KNNFit on the device
-    {
-        std::vector<int> Rs(static_cast<size_t>(nfr)), Nq(static_cast<size_t>(nfr));
-        std::vector<float> eps(static_cast<size_t>(nfr));
-        std::vector<size_t> coff(size_t(nfr) + 1, 0);
-        for (int i = 0; i < nfr; ++i) {
-            Rs[i] = frames[i].r;
-            Nq[i] = frames[i].n;
-            coff[i + 1] = coff[i] + size_t(frames[i].r) * cs;
-        }
-        // the queries Single(srcData) are already in HBM (device DSP)
-        std::vector<float> cand(coff[nfr]), q;
-        const int bd = opt_.chunk_bit_depth;
-        const int obd = (1 << (bd - 1)) - 1;
-        parallel_for(nfr, host_threads(), [&](int i) {
-            const FrameState& f = frames[i];
-            const double law = 1.0 / double(f.atten_div);
-            // epsilon (encoder.lpr:940-943), accumulated in Single
-            float acc = 1.0f;
-            for (int j = 0; j <= 15; ++j) acc = float(double(acc) + double(j) * law);
-            const float e1 = 1.0f / (float(1 << bd) * acc);
-            const float e2 = float(1.0 / 32767.0);
-            eps[i] = e1 > e2 ? e1 : e2;
-            float* cp = cand.data() + coff[i];
-            for (int c = 0; c < f.r; ++c) {
-                double coeff = 1.0;
-                for (int a = 0; a <= f.ratten[c]; ++a) coeff += double(a) * law;
-                for (int j = 0; j < cs; ++j) {
-                    double v = double(f.rdst[size_t(c) * cs + j]) / (double(obd) * coeff);
-                    v = std::min(1.0, std::max(-1.0, v));
-                    *cp++ = float(v);
-                }
+    int post_rc = 0;
+    if (batched_scan) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        std::thread worker([&] {
+            if (hipSetDevice(dev) != hipSuccess) {
+                post_err = "KNNFit/pack pipeline: hipSetDevice failed";
+                post_rc = -1;
+                return;
             }
+            post_rc = post_loop();
         });
-        std::vector<int> best;
-        t2c = now_ms();
-        if (run_knnfit_batch(cs, Rs, Nq, eps, cand, q, &best, &knn_ms, dQry.p) != 0) {
-            *err = t_err;
-            return -1;
+        std::vector<float> C;
+        std::vector<int> it, sl;
+        g_scan_rounds.store(0);
+        int* cl_dev = nullptr;
+        int* nt_dev = nullptr;
+        int rr = 0;
+        if (hipHostGetDevicePointer(reinterpret_cast<void**>(&cl_dev), cl_host, 0) != hipSuccess ||
+            hipHostGetDevicePointer(reinterpret_cast<void**>(&nt_dev), notify, 0) != hipSuccess) {
+            rr = fail("KNNScanReduce: no device address for the host-mapped cluster buffers");
+        } else {
+            rr = run_reduce_batch_dev(D, K, opt_.precision, Ns, red_xoff, dFeat.p, &C, &cl_final, &it, &sl, &restarts,
+                                      &yak_ms, &scan_ms, cl_dev, nt_dev);
         }
-        size_t off = 0;
-        for (int i = 0; i < nfr; ++i) {
-            frames[i].best.assign(best.begin() + long(off), best.begin() + long(off + size_t(frames[i].n)));
-            off += size_t(frames[i].n);
+        t_scan_end = now_ms();
+        if (rr != 0) *err = t_err;
+        scan_state.store(rr != 0 ? -1 : 1, std::memory_order_release);
+        worker.join();
+        if (rr != 0) return -1;
+        for (int j = 0; j < nred; ++j) {
+            FrameState& f = frames[size_t(red_idx[size_t(j)])];
+            f.scan_iters = it[size_t(j)];
+            f.scan_slow = sl[size_t(j)];
+            passes += it[size_t(j)];
+            slow += sl[size_t(j)];
         }
+    } else {
+        t_scan_end = now_ms();
+        scan_state.store(1, std::memory_order_release);
+        post_rc = post_loop();
     }
-    double t3 = now_ms();
-    parallel_for(nfr, host_threads(), [&](int i) {
-        frame_knnfit_post(frames[i]);
-        frame_save(frames[i]);
-    });
+    if (post_rc != 0) {
+        *err = post_err;
+        return -1;
+    }
+    const double t2 = t_scan_end;
+    const double t3 = now_ms();
     if (recon && device_recon(b, frames, recon, err) != 0) return -1;
     out->clear();
     for (auto& f : frames) out->insert(out->end(), f.stream.begin(), f.stream.end());
     double t4 = now_ms();
     if (std::getenv("GSC_HOST_TIMING"))
         std::fprintf(stderr,
-                     "host timing [ms]: frames+dsp %.1f (dsp %.1f) | reduce (yakmo %.1f scan %.1f) %.1f | reduce_post %.1f |"
-                     " knn_stage %.1f | knnfit call %.1f (kernel %.1f) | knn_post+save+concat %.1f\n",
-                     t1 - t0, dsp_ms, yak_ms, scan_ms, t2 - t1, t2b - t2, t2c - t2b, t3 - t2c, knn_ms, t4 - t3);
+                     "host timing [ms]: frames+dsp %.1f (dsp %.1f) | reduce (yakmo %.1f scan %.1f) %.1f |"
+                     " post after the scan %.1f (in the scan tail %.1f, KNNFit kernels %.1f, %d groups) | concat %.1f\n",
+                     t1 - t0, dsp_ms, yak_ms, scan_ms, t2 - t1, t3 - t2, overlap_ms, pc.knn_ms, pc.groups, t4 - t3);
     if (std::getenv("GSC_HOST_TIMING") && !red_idx.empty()) {  // per-frame pass counts (scan tail)
         std::vector<int> h(kMaxScanIters + 1, 0);
         for (int i : red_idx) h[std::min(kMaxScanIters, std::max(0, frames[i].scan_iters))]++;
@@ -827,8 +1188,10 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
         tim->gpu_dsp_ms = dsp_ms;
         tim->gpu_yakmo_ms = yak_ms;
         tim->gpu_scan_ms = scan_ms;
-        tim->gpu_knnfit_ms = knn_ms;
-        tim->host_post_ms = (t3 - t2 - knn_ms) + (t4 - t3);
+        tim->gpu_knnfit_ms = pc.knn_ms;
+        tim->host_post_ms = t4 - t2;  // what the post-processing adds after the scan
+        tim->post_overlap_ms = overlap_ms;
+        tim->post_groups = pc.groups;
         tim->frames = nfr;
         tim->reduce_frames = int(red_idx.size());
         long long pts = 0;
@@ -841,7 +1204,7 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
         for (auto& f : frames) pp += (long long)f.scan_iters * f.n;
         tim->scan_point_passes = pp;
         tim->scan_launches = g_scan_rounds.exchange(0);
-        tim->knnfit_launches = 1;
+        tim->knnfit_launches = pc.groups;
         long long cand = 0;
         for (auto& f : frames) cand += (long long)f.n * 4 * f.r_before_prune;
         tim->knnfit_pairs = cand;

@@ -1696,7 +1696,19 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         __threadfence();
         __syncthreads();
     }
-    if (done) break;
+    if (done) {
+        // hand the final clusters to the host's post-processing while the
+        // other frames still scan: a host-mapped copy, then the flag
+        int* clh = wg0 ? uniform_ptr(frp->cl_host) : nullptr;
+        if (clh) {
+            for (int j = tid; j < N; j += nthreads)
+                clh[j] = __hip_atomic_load(&clusters[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __threadfence_system();
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(uniform_ptr(frp->notify), 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        break;
+    }
     }
     }
 }

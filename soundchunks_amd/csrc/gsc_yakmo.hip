@@ -39,7 +39,30 @@ template <int D>
 constexpr int yakmo_per() {
     return 1;
 }
-constexpr int kYThreads = 64 + kYDist;   // wave 0: picks + prefix chain
+constexpr int kYThreads = 64 + kYDist;
+
+#ifdef GSC_STAMPS
+// diagnostic phase clocks (make stamps): s_memtime deltas per role
+__device__ __forceinline__ uint64_t ystamp() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define YST_DECL uint64_t yacc[16] = {}; uint64_t ylast = ystamp();
+#define YST(k)                     \
+    {                              \
+        const uint64_t t_ = ystamp(); \
+        yacc[k] += t_ - ylast;     \
+        ylast = t_;                \
+    }
+#define YCNT(k) yacc[k] += 1;
+#else
+#define YST_DECL
+#define YST(k)
+#define YCNT(k)
+#endif   // wave 0: picks + prefix chain
 constexpr int kYBits = 262144 / 32;   // chosen-point bitmap in LDS (N <= 262144)
 
 struct YakmoShared {
@@ -165,6 +188,7 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
     constexpr int BLK = kYDist * kYPer;  // points per pipeline step
     const int nblk = (N + BLK - 1) / BLK;
     const int dt = tid - 64;  // distance thread of waves 1..4 (negative on wave 0)
+    YST_DECL
     for (int i = 0; i < K; ++i) {
         // ---- pick (wave 0; the RNG runs redundantly in every thread)
         const uint64_t t = rx ^ (rx << 11);
@@ -207,11 +231,14 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
                 sh.c[lane] = v;
                 C[(int64_t)i * D + lane] = v;  // the seeds (C is overwritten by the means at the end)
             }
+            YST(0)
         }
         __syncthreads();
         const bool chain = i < K - 1;
         if (wave == 0) {
+            YST(3)
             __syncthreads();  // the distance waves' seed-distance table
+            YST(3)
             // sequential f32 prefix over the blocks as they complete (encoder's cum[], DLL @0x180001e74)
             float run = 0.0f;
             for (int b = 0; b <= nblk; ++b) {
@@ -219,7 +246,9 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
                     const int base = (b - 1) * BLK;
                     const float* rg = sh.ring[(b - 1) & 1];
                     if (base + BLK <= N && chain_step_binade<BLK / 64>(rg, ckpt + (base >> 6), lane, &run)) {
+                        YST(1) YCNT(4)
                         __syncthreads();
+                        YST(3)
                         continue;
                     }
                     for (int k = 0; k < BLK / 64; ++k) {
@@ -246,8 +275,10 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
                         }
                         if (lane == 0) ckpt[((base + k * 64) >> 6)] = run;
                     }
+                    YST(2) YCNT(5)
                 }
                 __syncthreads();
+                YST(3)
             }
             total = run;
         } else {
@@ -267,7 +298,9 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
                 }
                 sh.sdlo[a] = fm(s2, 0.99998474f);
             }
+            YST(8)
             __syncthreads();
+            YST(8)
             // Elkan skip: with E = (|x|^2 + cmax) 2^-16 >= the rounding error of any of the
             // DLL's expanded-form distances from x (< 80 u (|x|^2 + |c|^2)), the computed
             // d0 = d(x, c_a) and d(x, c_i) are within E of the true squares, so
@@ -348,10 +381,19 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
                         }
                     }
                 }
+                YST(9)
                 __syncthreads();
+                YST(10)
             }
         }
     }
+#ifdef GSC_STAMPS
+    if (tid == 0 || tid == 64) {
+        uint64_t* ys = const_cast<ReduceFrame*>(frames)[fi].ystamps;
+        for (int k = 0; k < 16; ++k)
+            if ((tid == 0) == (k < 8)) ys[k] = yacc[k];
+    }
+#endif
     // ---- means of the seeding assignment (@0x180002290): c = f32(sum in point order) / f32(count)
     int* counts = i_scratch + fr.k_off;
     for (int k = tid; k < K; k += kYThreads) sh.cursor[k] = 0;
