@@ -22,7 +22,7 @@
 #include "gsc_device.h"
 
 extern "C" hipError_t gsc_launch_yakmo(int D, const gsc::ReduceFrame* frames, int nframes, const float* X, float* C,
-                                       float* fs, int* is, uint32_t* bits, hipStream_t st);
+                                       float* fs, int* is, uint32_t* bits, int max_n, hipStream_t st);
 extern "C" hipError_t gsc_launch_ann_build(const float* pts, int n, int dd, int* pidx, int* cd, float* cv, float* lo,
                                            float* hi, float* bnd, hipStream_t st);
 extern "C" hipError_t gsc_launch_ann_query(const float* pts, int n, int dd, int* pidx, int* cd, float* cv, float* lo,
@@ -146,8 +146,8 @@ void yakmo_train_on_data(yakmo_t* ay, int* pointToCluster) {
     if (!ay) fatal(fn, "null handle");
     const int N = int(ay->rows), D = int(ay->cols), K = int(ay->k);
     if (!ay->supported) fatal(fn, "only yakmo_create(K,1,0,1,0,0,v) is implemented");
-    if (K <= 0 || K >= N || N > 262144 || !(D == 8 || D == 16 || D == 32))
-        fatal(fn, "unsupported shape (need 0 < K < N <= 262144, D in {8, 16, 32})");
+    if (K <= 0 || K >= N || K > gsc::kMaxK || N > 262144 || !(D == 8 || D == 16 || D == 32))
+        fatal(fn, "unsupported shape (need 0 < K < N <= 262144, K <= 4096, D in {8, 16, 32})");
     if (!device_ok()) fatal(fn, "no gfx950 device (the MI355X hot path has no CPU fallback)");
     gsc::ReduceFrame fr{};
     fr.N = N;
@@ -160,7 +160,7 @@ void yakmo_train_on_data(yakmo_t* ay, int* pointToCluster) {
     if (!dX.p || !dC.p || !dF.p || !dI.p || !dB.p || !dFr.p) fatal(fn, "device allocation failed");
     check(fn, hipMemcpy(dX.p, ay->data.data(), 4 * ay->data.size(), hipMemcpyHostToDevice));
     check(fn, hipMemcpy(dFr.p, &fr, sizeof(fr), hipMemcpyHostToDevice));
-    check(fn, gsc_launch_yakmo(D, dFr.p, 1, dX.p, dC.p, dF.p, dI.p, dB.p, nullptr));
+    check(fn, gsc_launch_yakmo(D, dFr.p, 1, dX.p, dC.p, dF.p, dI.p, dB.p, N, nullptr));
     ay->centroids.resize(size_t(K) * D);
     ay->labels.resize(size_t(N));
     check(fn, hipMemcpy(ay->centroids.data(), dC.p, 4 * ay->centroids.size(), hipMemcpyDeviceToHost));

@@ -25,7 +25,7 @@
 #include "gsc_encoder.h"
 
 extern "C" hipError_t gsc_launch_yakmo(int D, const gsc::ReduceFrame* frames, int nframes, const float* X, float* C,
-                                       float* fs, int* is, uint32_t* bits, hipStream_t st);
+                                       float* fs, int* is, uint32_t* bits, int max_n, hipStream_t st);
 extern "C" hipError_t gsc_launch_scan_pass(int D, gsc::ReduceFrame* frames, int nframes, int K, const float* X,
                                            float* C, int* is, float* fs, const float* rate_tab, double tol, int max_passes,
                                            int only_flagged, hipStream_t st);
@@ -282,7 +282,7 @@ int run_reduce_batch_dev(int D, int K, int precision, const std::vector<int>& Ns
     HIP_TRY(hipEventCreate(&e1));
     HIP_TRY(hipEventCreate(&e2));
     HIP_TRY(hipEventRecord(e0, nullptr));
-    HIP_TRY(gsc_launch_yakmo(D, dFr.p, nf, dX, dC.p, dF.p, dI.p, dBits.p, nullptr));
+    HIP_TRY(gsc_launch_yakmo(D, dFr.p, nf, dX, dC.p, dF.p, dI.p, dBits.p, int(maxN), nullptr));
     HIP_TRY(hipEventRecord(e1, nullptr));
     HIP_TRY(launch_scan_passes(D, dFr.p, nf, K, dX, dC.p, dI.p, dF.p, dRate.p, precision));
     HIP_TRY(hipEventRecord(e2, nullptr));
@@ -1441,7 +1441,7 @@ int gsc_encode_wav_recon(const uint8_t* wav, size_t wav_len, const gsc_options* 
 
 int gsc_yakmo_seed_means(int n, int d, const float* x, int k, float* centroids) {
     if (ensure_device() != 0) return -1;
-    if (k >= n || k <= 0) return fail("yakmo needs 0 < k < n");
+    if (k >= n || k <= 0 || k > kMaxK) return fail("yakmo needs 0 < k < n, k <= 4096");
     if (n > 262144) return fail("yakmo seeding supports at most 262144 points");
     std::vector<float> X(x, x + size_t(n) * d), C;
     std::vector<int> cl, it, sl;
@@ -1465,7 +1465,7 @@ int gsc_yakmo_seed_means(int n, int d, const float* x, int k, float* centroids) 
     HIP_TRY(dFr.alloc(1));
     HIP_TRY(hipMemcpy(dX.p, X.data(), sizeof(float) * X.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(dFr.p, fr.data(), sizeof(ReduceFrame), hipMemcpyHostToDevice));
-    HIP_TRY(gsc_launch_yakmo(d, dFr.p, nf, dX.p, dC.p, dF.p, dI.p, dBits.p, nullptr));
+    HIP_TRY(gsc_launch_yakmo(d, dFr.p, nf, dX.p, dC.p, dF.p, dI.p, dBits.p, n, nullptr));
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(centroids, dC.p, sizeof(float) * size_t(k) * d, hipMemcpyDeviceToHost));
     (void)C;

@@ -7,18 +7,18 @@
 // Per pick i the DLL walks every point once: d = ((|c|^2 + |x|^2) + 0) -
 // sum_j (2 x_j) c_j (f32, dimension order), keeps the nearest seed (strict
 // <) and, for i < K-1, the running f32 total cum[n] that the next pick's
-// lower_bound searches.  That prefix is one sequential f32 chain per pick;
-// here wave 0 runs it through 64-element registers (readlane + add) while
-// the other waves compute the next block's distances.  Only every 64th cum is
-// stored (a checkpoint); lower_bound replays the chain from the checkpoint
-// below each probe, which reproduces cum exactly (same adds, same order) and
-// therefore the DLL's probe sequence even where tiny negative d make cum
-// non-monotone.
+// lower_bound searches.  That prefix is one sequential f32 chain per pick.
 //
-// Roles: wave 0 only picks and chains (the prefix, an integer prefix sum per
-// binade where that is exact, see chain_step_binade); waves 1..8 compute the distances of one
-// 2048-point block per step (4 points per thread), with the next block's loads issued a step ahead so
-// HBM latency hides under the chain.
+// Roles: wave 0 picks and chains; waves 1..8 compute one 512-point block per
+// step (one point per thread), d0 and seed ids prefetched eight steps ahead and
+// the X rows of points that the Elkan bound cannot skip two steps ahead.
+// The chain turns each run of whole 64-point blocks into one integer prefix
+// sum while the total stays in one binade (chain_fast: exact, or the blocks
+// are added one by one), and keeps per 64-point block the checkpoint cum and
+// the block's min / max in LDS.  The next pick's lower_bound then finds its
+// block from the maxima and proves from the minima that the DLL's binary
+// search cannot end anywhere else (pick_lower_bound), replaying one block;
+// where it cannot prove that, it replays the DLL's probe sequence.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -31,15 +31,16 @@ __device__ __forceinline__ float fa(float a, float b) { return __fadd_rn(a, b); 
 __device__ __forceinline__ float fs(float a, float b) { return __fsub_rn(a, b); }
 __device__ __forceinline__ float fm(float a, float b) { return __fmul_rn(a, b); }
 
-constexpr int kYDist = 512;            // distance threads (waves 1..8)
-constexpr int kYBlock = kYDist * 4;    // largest step (points): ring size
-// points per distance thread per step (loads in flight), bounded by the VGPR
-// budget of 9 waves (168): 4 rows of D = 8, 2 of D = 16, 1 of D = 32
-template <int D>
-constexpr int yakmo_per() {
-    return 1;
-}
-constexpr int kYThreads = 64 + kYDist;
+constexpr int kYDist = 512;            // distance threads (8 waves)
+constexpr int kYBlock = kYDist;        // points per pipeline step: one per distance thread
+// 12 waves, 3 per SIMD: wave 0 picks and chains; waves 4, 8 and 11 only keep
+// the barriers, so SIMD 0 issues the chain alone; the other 8 compute distances
+constexpr int kYThreads = 768;
+__device__ __forceinline__ bool yakmo_idle_wave(int w) { return w == 4 || w == 8 || w == 11; }
+// distance thread index of a distance wave's lane
+__device__ __forceinline__ int yakmo_dist_index(int w, int lane) { return (w - 1 - w / 4) * 64 + lane; }
+constexpr int kYBits = 262144 / 32;   // chosen-point bitmap in LDS (N <= 262144)
+constexpr int kYPre = 8;              // d0 / seed-id prefetch depth (steps); X rows: 2
 
 #ifdef GSC_STAMPS
 // diagnostic phase clocks (make stamps): s_memtime deltas per role
@@ -62,8 +63,7 @@ __device__ __forceinline__ uint64_t ystamp() {
 #define YST_DECL
 #define YST(k)
 #define YCNT(k)
-#endif   // wave 0: picks + prefix chain
-constexpr int kYBits = 262144 / 32;   // chosen-point bitmap in LDS (N <= 262144)
+#endif
 
 struct YakmoShared {
     alignas(16) float ring[2][kYBlock];    // d0 of the last two blocks (chain input)
@@ -73,33 +73,73 @@ struct YakmoShared {
         float sdlo[kMaxK];     // picks: lower bound of |c_i - c_a|^2 per earlier seed a
     };
     float c[32];               // current seed
+    float cn;                  // its |c|^2
     float cmax;                // max |c_a|^2 over the seeds so far
-    int idx;
-    float total;
+    float xmax;                // max |x|^2 over the frame's points
 };
+// dynamic LDS after YakmoShared, per 64-point block g of the current pick's
+// prefix cum[]: ck[g] = cum at the block's last point, bmn/bmx[g] = min/max of
+// the block's cum values
+
+// Barrier for LDS hand-offs only: the global loads in flight (the distance
+// waves' prefetch) stay in flight, which __syncthreads' full fence would drain.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// step barrier: LDS only, except the last step of a pick, which also orders
+// the pick's global d0 / seed-id / seed stores before the next pick reads them
+__device__ __forceinline__ void step_barrier(bool last) {
+    if (last)
+        __syncthreads();
+    else
+        lds_barrier();
+}
+
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
 
 // cum[m] of the current pick, replayed from the checkpoint below m (wave 0, all lanes)
-__device__ __forceinline__ float cum_at(const float* __restrict__ d0, const float* __restrict__ ckpt, int m, int lane) {
+__device__ __forceinline__ float cum_at(const float* __restrict__ d0, const float* ck, int m, int lane) {
     const int blk = m >> 6;
-    float run = blk > 0 ? ckpt[blk - 1] : 0.0f;
+    float run = blk > 0 ? ck[blk - 1] : 0.0f;
     const float v = d0[(blk << 6) + lane];  // m < N, so the block's first m - 64*blk + 1 loads are in range
     const int last = m & 63;
-    for (int l = 0; l <= last; ++l) run = fa(run, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)));
+    for (int l = 0; l <= last; ++l) run = fa(run, readlane_f(v, l));
     return run;
 }
 
-// Inclusive wave64 prefix sum of 32-bit integers (wrap-around arithmetic).
-__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t x, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-        if (lane >= d) x += y;
-    }
+// Inclusive wave64 prefix sum of 32-bit integers (wrap-around) by DPP:
+// row_shr 1/2/4/8 inside each row of 16, then row_bcast:15 / row_bcast:31
+// carry the row totals into the rows above.
+__device__ __forceinline__ uint32_t wave_scan_u32(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
     return x;
 }
 
-// One 256-point step of the sequential f32 prefix cum[n] = fl(cum[n-1] + d[n])
-// without the dependent add chain, exact or not at all.
+// min / max over the 8 lanes of an aligned lane octet (DPP: quad_perm
+// [1,0,3,2], [2,3,0,1], then row_half_mirror across the two quads)
+__device__ __forceinline__ uint32_t oct_min_u32(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xb1, 0xf, 0xf, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4e, 0xf, 0xf, false));
+    return min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false));
+}
+__device__ __forceinline__ uint32_t oct_max_u32(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xb1, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4e, 0xf, 0xf, false));
+    return max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false));
+}
+
+// The sequential f32 prefix cum[n] = fl(cum[n-1] + d[n]) over whole 64-point
+// blocks without the dependent add chain, exact or not at all.
 //
 // While the running total stays in one binade [2^e, 2^(e+1)), every partial
 // sum is a multiple of u = 2^(e-23): run = m*u with m in [2^23, 2^24).  Then
@@ -109,85 +149,240 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t x, int lane) {
 // (the sum stays in the binade, so its rounding grid is still u).  Under
 // those conditions the chain is an integer prefix sum: the d/u roundings are
 // independent of each other and of the order, and the integer sums are exact.
-// The step takes the fast path only when every point meets the conditions
-// (no tie, |d/u| < 2^24, every partial m + n_0 + ... + n_k in range);
-// otherwise it returns false and the caller adds the step point by point.
-// run must be a positive normal f32 (a zero or subnormal total has a
-// different grid).  Writes the NB 64-point checkpoints and the new run.
-template <int NB>
-__device__ __forceinline__ bool chain_step_binade(const float* __restrict__ ring, float* __restrict__ ck, int lane,
-                                                  float* run_io) {
+//
+// Points s .. s + 64 nbk - 1 of the ring (nbk <= 8 blocks, s a multiple of
+// 64); lane l takes 8 consecutive points: one local prefix, one wave scan.
+// The blocks before the first point that breaks a condition (tie, |d/u| >=
+// 2^24, a partial out of range) are accepted: their checkpoints and min/max
+// are written (global block index g0 + k) and *run_io moves to the last
+// accepted partial.  Returns the accepted block count.  run must be at least
+// 2^-100, so that 2^sc is a normal f32 and d * 2^sc is exact wherever it
+// matters (a d/u far below 1/2 may round: it still rounds to 0, no tie).
+__device__ __forceinline__ int chain_fast(const float* __restrict__ ring, int s, int nbk, int lane, float* run_io,
+                                          float* ck, float* bmn, float* bmx, int g0) {
     const float run = *run_io;
-    if (!(run >= 1.17549435e-38f)) return false;  // zero, negative, subnormal (or NaN)
+    if (!(run >= 7.88860905e-31f)) return 0;  // below 2^-100, zero, negative (or NaN)
     const int fe = __builtin_amdgcn_frexp_expf(run);  // run = f * 2^fe, f in [0.5, 1)
-    const int sc = 24 - fe;                          // d/u = d * 2^sc
-    const uint32_t m0 = (uint32_t)__builtin_ldexpf(run, sc);  // in [2^23, 2^24), exact
-    uint32_t p[NB];
-    bool good = true;
+    const int sc = 24 - fe;                          // d/u = d * 2^sc, sc <= 124
+    const float scale = __builtin_ldexpf(1.0f, sc), unscale = __builtin_ldexpf(1.0f, -sc);
+    const uint32_t m0 = (uint32_t)(run * scale);  // in [2^23, 2^24), exact
+    const bool act = lane < nbk * 8;
+    float v[8];
+    if (act) {
+        const float4 a = *reinterpret_cast<const float4*>(&ring[s + 8 * lane]);
+        const float4 b = *reinterpret_cast<const float4*>(&ring[s + 8 * lane + 4]);
+        v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
+    } else {
 #pragma unroll
-    for (int k = 0; k < NB; ++k) {
-        const float t = __builtin_ldexpf(ring[k * 64 + lane], sc);  // exact unless |t| is far below 1/2
-        const bool ok = __builtin_fabsf(t) < 16777216.0f && (t - __builtin_floorf(t)) != 0.5f;  // NaN: not ok
-        good &= ok;
-        p[k] = (uint32_t)(int)(ok ? __builtin_rintf(t) : 0.0f);
+        for (int e = 0; e < 8; ++e) v[e] = 0.0f;
     }
+    uint32_t q[8], acc = 0;
+    bool ok[8];
 #pragma unroll
-    for (int k = 0; k < NB; ++k) p[k] = wave_incl_scan_u32(p[k], lane);
-    uint32_t off = m0;
+    for (int e = 0; e < 8; ++e) {
+        const float t = v[e] * scale;
+        const float n = __builtin_rintf(t);
+        ok[e] = __builtin_fabsf(t) < 16777216.0f && __builtin_fabsf(t - n) != 0.5f;  // NaN: not ok
+        acc += (uint32_t)(int)n;  // garbage where !ok: that point fails below anyway
+        q[e] = acc;
+    }
+    const uint32_t base = m0 + (wave_scan_u32(acc) - acc);
+    uint64_t bad[8], anyb = 0;
 #pragma unroll
-    for (int k = 0; k < NB; ++k) {
-        const uint32_t v = off + p[k];
-        // m + partial in [2^23 + 1, 2^24 - 2]: then the exact sum, within 1/2 of
+    for (int e = 0; e < 8; ++e) {
+        q[e] += base;
+        // m + partial in [2^23 + 1, 2^24 - 2]: the exact sum, within 1/2 of
         // it, lies strictly inside the binade and rounds on the grid u
-        good &= (v - 8388609u) < 8388606u;
-        off = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-        p[k] = off;  // the block's last partial: its checkpoint
+        bad[e] = __ballot(act && !(ok[e] && (q[e] - 8388609u) < 8388606u));
+        anyb |= bad[e];
     }
-    if (__ballot(!good) != 0ull) return false;
+    int k = nbk;
+    if (anyb) {
+        const int L = __builtin_ctzll(anyb);
+        int e0 = 7;
 #pragma unroll
-    for (int k = 0; k < NB; ++k)
-        if (lane == 0) ck[k] = __builtin_ldexpf((float)p[k], -sc);  // exact: m < 2^24, same binade
-    *run_io = __builtin_ldexpf((float)off, -sc);
-    return true;
+        for (int e = 7; e >= 0; --e)
+            if ((bad[e] >> L) & 1ull) e0 = e;
+        k = min(nbk, (L * 8 + e0) >> 6);
+    }
+    if (k == 0) return 0;
+    uint32_t mn = q[0], mx = q[0];
+#pragma unroll
+    for (int e = 1; e < 8; ++e) {
+        mn = min(mn, q[e]);
+        mx = max(mx, q[e]);
+    }
+    mn = oct_min_u32(mn);  // in range, so integer order is the partials' order
+    mx = oct_max_u32(mx);
+    const int blk = lane >> 3;
+    if (blk < k) {
+        if ((lane & 7) == 0) {
+            bmn[g0 + blk] = (float)mn * unscale;  // exact: < 2^24, same binade
+            bmx[g0 + blk] = (float)mx * unscale;
+        }
+        if ((lane & 7) == 7) ck[g0 + blk] = (float)q[7] * unscale;
+    }
+    *run_io = (float)(uint32_t)__builtin_amdgcn_readlane((int)q[7], 8 * k - 1) * unscale;
+    return k;
+}
+
+// c <= 64 points of the ring from s added one by one (the reference's chain)
+__device__ __forceinline__ void chain_seq(const float* __restrict__ ring, int s, int c, int lane, float* run_io,
+                                          float* ck, float* bmn, float* bmx, int g) {
+    float run = *run_io, mn = 3.4028235e38f, mx = -3.4028235e38f;
+    if (c == 64) {
+        // the values as LDS broadcast reads into VGPRs (every lane loads the
+        // same row, 16 at a time, the next 16 in flight), then the dependent
+        // adds back to back
+        const float4* row = reinterpret_cast<const float4*>(&ring[s]);
+        float4 sv[4], nx[4];
+#pragma unroll
+        for (int l = 0; l < 4; ++l) sv[l] = row[l];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            if (h < 3) {
+#pragma unroll
+                for (int l = 0; l < 4; ++l) nx[l] = row[4 * (h + 1) + l];
+            }
+#pragma unroll
+            for (int l = 0; l < 4; ++l) {
+                run = fa(run, sv[l].x);
+                mn = fminf(mn, run), mx = fmaxf(mx, run);
+                run = fa(run, sv[l].y);
+                mn = fminf(mn, run), mx = fmaxf(mx, run);
+                run = fa(run, sv[l].z);
+                mn = fminf(mn, run), mx = fmaxf(mx, run);
+                run = fa(run, sv[l].w);
+                mn = fminf(mn, run), mx = fmaxf(mx, run);
+            }
+#pragma unroll
+            for (int l = 0; l < 4; ++l) sv[l] = nx[l];
+        }
+    } else {
+        const float v = lane < c ? ring[s + lane] : 0.0f;
+        for (int l = 0; l < c; ++l) {
+            run = fa(run, readlane_f(v, l));
+            mn = fminf(mn, run), mx = fmaxf(mx, run);
+        }
+    }
+    if (lane == 0) {
+        ck[g] = run;
+        bmn[g] = mn;
+        bmx[g] = mx;
+    }
+    *run_io = run;
+}
+
+// std::lower_bound(cum, cum + N, target) of the DLL's pick (@0x180001b20).
+// The probe sequence matters only where cum is not partitioned by target
+// (cum dips when a d0 is negative, e.g. a seed's own expanded-form distance).
+// If every cum before i* = the first index with cum >= target is below target
+// (true by definition) and every cum from i* on is >= target, any binary
+// search returns i*.  i*'s block is the first whose max reaches target; the
+// blocks after it are checked by their minima, i*'s own block by replaying it
+// from its checkpoint.  Otherwise (or with a non-finite total) the DLL's probe
+// sequence is replayed exactly.
+__device__ int pick_lower_bound(float target, float total, int N, const float* ck, const float* bmn, const float* bmx,
+                                const float* __restrict__ d0, int lane) {
+    const int nb = (N + 63) >> 6;
+    if (__builtin_isfinite(total)) {
+        int bstar = -1;
+        float suf = 3.4028235e38f;
+        for (int c0 = 0; c0 < nb; c0 += 64) {
+            const int g = c0 + lane;
+            const bool valid = g < nb;
+            if (bstar < 0) {
+                const uint64_t m = __ballot(valid && bmx[g] >= target);
+                if (m) bstar = c0 + __builtin_ctzll(m);
+            }
+            if (bstar >= 0 && valid && g > bstar) suf = fminf(suf, bmn[g]);
+        }
+        if (bstar < 0) return N;  // every cum < target
+        suf = fminf(suf, __shfl_xor(suf, 1, 64));
+        suf = fminf(suf, __shfl_xor(suf, 2, 64));
+        suf = fminf(suf, __shfl_xor(suf, 4, 64));
+        suf = fminf(suf, __shfl_xor(suf, 8, 64));
+        suf = fminf(suf, __shfl_xor(suf, 16, 64));
+        suf = fminf(suf, __shfl_xor(suf, 32, 64));
+        if (suf >= target) {
+            const int base = bstar << 6, c = min(64, N - base);
+            const float v = lane < c ? d0[base + lane] : 0.0f;
+            float run = bstar > 0 ? ck[bstar - 1] : 0.0f, mine = 0.0f;
+            for (int l = 0; l < c; ++l) {
+                run = fa(run, readlane_f(v, l));
+                if (lane == l) mine = run;
+            }
+            const uint64_t ge = __ballot(lane < c && mine >= target);
+            if (ge) {
+                const int j = __builtin_ctzll(ge);
+                if (__ballot(lane >= j && lane < c && !(mine >= target)) == 0ull) return base + j;
+            }
+        }
+    }
+    int first = 0, count = N;
+    while (count > 0) {
+        const int half = count >> 1;
+        const int mid = first + half;
+        if (target > cum_at(d0, ck, mid, lane)) {
+            first = mid + 1;
+            count -= half + 1;
+        } else {
+            count = half;
+        }
+    }
+    return first;
 }
 
 }  // namespace
+
+// dynamic LDS bytes of a frame with N points
+__host__ __device__ constexpr size_t yakmo_dyn_lds(int N) { return size_t(3) * size_t((N + 63) / 64) * sizeof(float); }
 
 template <int D>
 __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFrame* __restrict__ frames, int nframes,
                                                                  const float* __restrict__ Xall, float* __restrict__ Call,
                                                                  float* __restrict__ f_scratch, int* __restrict__ i_scratch) {
     __shared__ YakmoShared sh;
+    extern __shared__ __attribute__((aligned(16))) float ydyn[];
     const int fi = blockIdx.x;
     if (fi >= nframes) return;
     const ReduceFrame fr = frames[fi];
     const int N = fr.N, K = fr.K;
+    const int nb = (N + 63) >> 6;
+    float* ck = ydyn;
+    float* bmn = ydyn + nb;
+    float* bmx = ydyn + 2 * nb;
     const float* __restrict__ X = Xall + fr.x_off;
     float* C = Call + fr.c_off;
     float* d0 = f_scratch + fr.n_off * 4;
     float* norm = d0 + N;
-    float* ckpt = norm + N;          // N/64 + 1 checkpoints
-    int* order = reinterpret_cast<int*>(ckpt + (N >> 6) + 1);  // N point indices (cluster order)
+    int* order = reinterpret_cast<int*>(norm + N);  // N point indices (cluster order)
+    uint16_t* id16 = reinterpret_cast<uint16_t*>(order + N);  // seed of each point (K <= 4096), the picks' copy
     int* idv = i_scratch + fr.n_off;  // seeding assignment
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
     // yakmo point norm: norm += v*v (f32, in order) (@0x1800015cb)
+    float xm = 0.0f;
     for (int n = tid; n < N; n += kYThreads) {
         const float* x = X + (int64_t)n * D;
         float s = 0.0f;
 #pragma unroll
         for (int j = 0; j < D; ++j) s = fa(s, fm(x[j], x[j]));
         norm[n] = s;
+        xm = fmaxf(xm, __builtin_isnan(s) ? 3.4028235e38f : s);
     }
     for (int w = tid; w < kYBits; w += kYThreads) sh.chosen[w] = 0u;
+    if (tid == 0) sh.xmax = 0.0f;
+    __syncthreads();
+    atomicMax(reinterpret_cast<unsigned*>(&sh.xmax), __float_as_uint(xm));  // non-negative floats order as integers
     __syncthreads();
 
     uint64_t rx = 123456789ull, ry = 362436069ull, rz = 521288629ull, rw = 88675123ull;
     float total = 0.0f;
-    constexpr int kYPer = yakmo_per<D>();
-    constexpr int BLK = kYDist * kYPer;  // points per pipeline step
+    constexpr int BLK = kYBlock;
     const int nblk = (N + BLK - 1) / BLK;
-    const int dt = tid - 64;  // distance thread of waves 1..4 (negative on wave 0)
+    const bool idle = yakmo_idle_wave(wave);
+    const int dt = (wave == 0 || idle) ? -1 : yakmo_dist_index(wave, lane);  // distance thread index
     YST_DECL
     for (int i = 0; i < K; ++i) {
         // ---- pick (wave 0; the RNG runs redundantly in every thread)
@@ -197,25 +392,27 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
         rz = rw;
         rw = rw ^ (rw >> 19) ^ t ^ (t >> 8);
         const float r = (float)((double)rw * 5.42101086242752217e-20);  // f32(f64(w) * 2^-64)
+        // distance waves: this pick's first seed ids / d0 are in flight during the pick
+        float pd[kYPre];
+        int pa[kYPre];
+        if (dt >= 0) {
+#pragma unroll
+            for (int q = 0; q < kYPre; ++q) {
+                const int n = q * BLK + dt;
+                pd[q] = 0.0f;
+                pa[q] = 0;
+                if (i > 0 && n < N) {
+                    pd[q] = d0[n];
+                    pa[q] = id16[n];
+                }
+            }
+        }
         if (wave == 0) {
             uint32_t idx;
             if (i == 0) {
                 idx = (uint32_t)(int64_t)floorf(fm(r, (float)N));
             } else {
-                // std::lower_bound(cum, cum + N, r * total): r*total > cum[mid] moves right
-                const float target = fm(r, total);
-                int first = 0, count = N;
-                while (count > 0) {
-                    const int half = count >> 1;
-                    const int mid = first + half;
-                    if (target > cum_at(d0, ckpt, mid, lane)) {
-                        first = mid + 1;
-                        count -= half + 1;
-                    } else {
-                        count = half;
-                    }
-                }
-                idx = (uint32_t)(int64_t)(float)first;
+                idx = (uint32_t)(int64_t)(float)pick_lower_bound(fm(r, total), total, N, ck, bmn, bmx, d0, lane);
             }
             // collision walk (@0x180001b20) and clamp (@0x180001c50)
             while (idx < (uint32_t)N && ((sh.chosen[idx >> 5] >> (idx & 31)) & 1u))
@@ -223,8 +420,9 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
             if (idx >= (uint32_t)N) idx = (uint32_t)(N - 1);
             if (lane == 0) {
                 sh.chosen[idx >> 5] |= 1u << (idx & 31);
-                sh.idx = (int)idx;
-                sh.cmax = i == 0 ? norm[idx] : fmaxf(sh.cmax, norm[idx]);
+                const float cn = norm[idx];
+                sh.cn = cn;
+                sh.cmax = i == 0 ? cn : fmaxf(sh.cmax, cn);
             }
             if (lane < D) {
                 const float v = X[(int64_t)idx * D + lane];
@@ -233,11 +431,11 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
             }
             YST(0)
         }
-        __syncthreads();
+        lds_barrier();  // the seed (LDS); its C row is read from the next pick on
         const bool chain = i < K - 1;
         if (wave == 0) {
             YST(3)
-            __syncthreads();  // the distance waves' seed-distance table
+            lds_barrier();  // the distance waves' seed-distance table
             YST(3)
             // sequential f32 prefix over the blocks as they complete (encoder's cum[], DLL @0x180001e74)
             float run = 0.0f;
@@ -245,48 +443,36 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
                 if (chain && b > 0) {
                     const int base = (b - 1) * BLK;
                     const float* rg = sh.ring[(b - 1) & 1];
-                    if (base + BLK <= N && chain_step_binade<BLK / 64>(rg, ckpt + (base >> 6), lane, &run)) {
-                        YST(1) YCNT(4)
-                        __syncthreads();
-                        YST(3)
-                        continue;
-                    }
-                    for (int k = 0; k < BLK / 64; ++k) {
-                        const int cnt = min(64, N - (base + k * 64));
-                        if (cnt <= 0) break;
-                        if (cnt == 64) {
-                            // the 64 values as LDS broadcast reads into VGPRs (every lane loads
-                            // the same row), then the dependent adds back to back: no VALU
-                            // readlane per point on the critical chain
-                            const float4* row = reinterpret_cast<const float4*>(&rg[k * 64]);
-                            float4 sv[16];
-#pragma unroll
-                            for (int l = 0; l < 16; ++l) sv[l] = row[l];
-#pragma unroll
-                            for (int l = 0; l < 16; ++l) {
-                                run = fa(run, sv[l].x);
-                                run = fa(run, sv[l].y);
-                                run = fa(run, sv[l].z);
-                                run = fa(run, sv[l].w);
-                            }
-                        } else {
-                            const int v = __float_as_int(rg[k * 64 + lane]);
-                            for (int l = 0; l < cnt; ++l) run = fa(run, __int_as_float(__builtin_amdgcn_readlane(v, l)));
+                    const int cnt = min(BLK, N - base);
+                    int s = 0;
+                    while (s < cnt) {
+                        const int full = (cnt - s) >> 6;
+                        if (full > 0) {
+                            const int k = chain_fast(rg, s, full, lane, &run, ck, bmn, bmx, (base + s) >> 6);
+                            s += k << 6;
+                            YST(1) YCNT(4)
+                            if (s >= cnt) break;
                         }
-                        if (lane == 0) ckpt[((base + k * 64) >> 6)] = run;
+                        // the block at s breaks a fast-path condition (or is the last, partial one)
+                        const int c = min(64, cnt - s);
+                        chain_seq(rg, s, c, lane, &run, ck, bmn, bmx, (base + s) >> 6);
+                        s += c;
+                        YST(2) YCNT(5)
                     }
-                    YST(2) YCNT(5)
                 }
-                __syncthreads();
+                step_barrier(b == nblk);
                 YST(3)
             }
             total = run;
+        } else if (idle) {
+            lds_barrier();
+            for (int b = 0; b <= nblk; ++b) step_barrier(b == nblk);
         } else {
             float c[D];
 #pragma unroll
             for (int j = 0; j < D; ++j) c[j] = sh.c[j];
-            const float cn = norm[sh.idx];
-            const float cmax = sh.cmax;
+            const float cn = sh.cn;
+            const float cmax = sh.cmax, xmax = sh.xmax;
             // Seed-distance table: sdlo[a] <= |c_i - c_a|^2 (the f32 sum of squared
             // differences, lowered by 2^-16 relative to cover its rounding).
             for (int a = dt; a < i; a += kYDist) {
@@ -299,91 +485,81 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
                 sh.sdlo[a] = fm(s2, 0.99998474f);
             }
             YST(8)
-            __syncthreads();
+            lds_barrier();
             YST(8)
-            // Elkan skip: with E = (|x|^2 + cmax) 2^-16 >= the rounding error of any of the
-            // DLL's expanded-form distances from x (< 80 u (|x|^2 + |c|^2)), the computed
-            // d0 = d(x, c_a) and d(x, c_i) are within E of the true squares, so
+            // Elkan skip: with E = (max|x|^2 + cmax) 2^-16 >= the rounding error of any of
+            // the DLL's expanded-form distances from x (< 80 u (|x|^2 + |c|^2)), the
+            // computed d0 = d(x, c_a) and d(x, c_i) are within E of the true squares, so
             // |c_i - c_a| >= 2 sqrt(max(d0, 0) + E) implies d(x, c_i) >= d0: no strict
             // improvement, and the point's X row need not be read for this pick.
-            auto skip_of = [&](float dold, float xn, int a) -> bool {
+            const float e = fm(fa(xmax, cmax), 1.52587891e-05f);
+            auto skip_of = [&](float dold, int a) -> bool {
                 if (i == 0) return false;
-                const float e = fm(fa(xn, cmax), 1.52587891e-05f);
                 const float need = fm(fm(fa(fmaxf(dold, 0.0f), e), 4.0f), 1.00000381f);
                 return sh.sdlo[a] >= need;
             };
-            // one pass over the points: d0/id update; block b+1's X rows (when not
-            // skipped) and block b+2's d0/|x|^2/id are loaded during step b.  Each
-            // thread owns kYPer points per block (kYDist apart, coalesced).
-            float xv[kYPer][D];
-            float xn[kYPer], dold[kYPer], xn_n[kYPer], dold_n[kYPer];
-            bool skip[kYPer];
-            int a_n[kYPer];
+            // pipeline: step b computes block b; the X rows of block b + XD (when
+            // not skipped) and the d0 / seed ids of block b + 8 are loaded meanwhile
+            constexpr int XD = D == 32 ? 1 : 2;  // X-row look-ahead (VGPR budget of 9 waves)
+            float xv[XD][D];
+            bool skip[XD];
 #pragma unroll
-            for (int q = 0; q < kYPer; ++q) {
-                const int n0 = q * kYDist + dt, n1 = n0 + BLK;
-                xn[q] = 0.0f;
-                dold[q] = 0.0f;
+            for (int q = 0; q < XD; ++q) {
+                const int n = q * BLK + dt;
                 skip[q] = true;
-                if (n0 < N) {
-                    xn[q] = norm[n0];
-                    dold[q] = d0[n0];
-                    skip[q] = skip_of(dold[q], xn[q], i == 0 ? 0 : idv[n0]);
+                if (n < N) {
+                    skip[q] = skip_of(pd[q], pa[q]);
                     if (!skip[q]) {
 #pragma unroll
-                        for (int j = 0; j < D; ++j) xv[q][j] = X[(int64_t)n0 * D + j];
+                        for (int j = 0; j < D; ++j) xv[q][j] = X[(int64_t)n * D + j];
                     }
                 }
-                xn_n[q] = 0.0f;
-                dold_n[q] = 0.0f;
-                a_n[q] = 0;
-                if (n1 < N) {
-                    xn_n[q] = norm[n1];
-                    dold_n[q] = d0[n1];
-                    a_n[q] = i == 0 ? 0 : idv[n1];
-                }
             }
-            for (int b = 0; b <= nblk; ++b) {
+            for (int b0 = 0; b0 <= nblk; b0 += kYPre) {
 #pragma unroll
-                for (int q = 0; q < kYPer; ++q) {
-                    const int n = b * BLK + q * kYDist + dt;
+                for (int u = 0; u < kYPre; ++u) {
+                    const int b = b0 + u;
+                    if (b > nblk) break;
+                    const int s2 = u % XD;
+                    const int n = b * BLK + dt;
                     if (b < nblk && n < N) {
-                        float dn = dold[q];
-                        if (!skip[q]) {
-                            float d = fa(fa(cn, xn[q]), 0.0f);
+                        float dn = pd[u];
+                        if (!skip[s2]) {
+                            float xn = 0.0f;  // yakmo's |x|^2, as computed at the start
 #pragma unroll
-                            for (int j = 0; j < D; ++j) d = fs(d, fm(fa(xv[q][j], xv[q][j]), c[j]));
+                            for (int j = 0; j < D; ++j) xn = fa(xn, fm(xv[s2][j], xv[s2][j]));
+                            float d = fa(fa(cn, xn), 0.0f);
+#pragma unroll
+                            for (int j = 0; j < D; ++j) d = fs(d, fm(fa(xv[s2][j], xv[s2][j]), c[j]));
                             if (i == 0 || dn > d) {
                                 dn = d;
                                 d0[n] = d;
                                 idv[n] = i;
+                                id16[n] = (uint16_t)i;
                             }
                         }
-                        sh.ring[b & 1][q * kYDist + dt] = dn;
+                        sh.ring[b & 1][dt] = dn;
                     }
-                }
+                    // block b + XD: skip decision and X rows (slot s2 is free now)
+                    const int n2 = n + XD * BLK;
+                    skip[s2] = true;
+                    if (b + XD < nblk && n2 < N) {
+                        skip[s2] = skip_of(pd[(u + XD) % kYPre], pa[(u + XD) % kYPre]);
+                        if (!skip[s2]) {
 #pragma unroll
-                for (int q = 0; q < kYPer; ++q) {
-                    const int n2 = (b + 1) * BLK + q * kYDist + dt;
-                    if (b + 1 < nblk && n2 < N) {
-                        xn[q] = xn_n[q];
-                        dold[q] = dold_n[q];
-                        skip[q] = skip_of(dold[q], xn[q], a_n[q]);
-                        if (!skip[q]) {
-#pragma unroll
-                            for (int j = 0; j < D; ++j) xv[q][j] = X[(int64_t)n2 * D + j];
-                        }
-                        const int n3 = n2 + BLK;
-                        if (b + 2 < nblk && n3 < N) {
-                            xn_n[q] = norm[n3];
-                            dold_n[q] = d0[n3];
-                            a_n[q] = i == 0 ? 0 : idv[n3];
+                            for (int j = 0; j < D; ++j) xv[s2][j] = X[(int64_t)n2 * D + j];
                         }
                     }
+                    // block b + kYPre: d0 and seed id (slot u is free now)
+                    const int n4 = n + kYPre * BLK;
+                    if (i > 0 && b + kYPre < nblk && n4 < N) {
+                        pd[u] = d0[n4];
+                        pa[u] = id16[n4];
+                    }
+                    YST(9)
+                    step_barrier(b == nblk);
+                    YST(10)
                 }
-                YST(9)
-                __syncthreads();
-                YST(10)
             }
         }
     }
@@ -394,7 +570,7 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
             if ((tid == 0) == (k < 8)) ys[k] = yacc[k];
     }
 #endif
-    // ---- means of the seeding assignment (@0x180002290): c = f32(sum in point order) / f32(count)
+// ---- means of the seeding assignment (@0x180002290): c = f32(sum in point order) / f32(count)
     int* counts = i_scratch + fr.k_off;
     for (int k = tid; k < K; k += kYThreads) sh.cursor[k] = 0;
     __syncthreads();
@@ -444,12 +620,22 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
 using namespace gsc;
 
 extern "C" hipError_t gsc_launch_yakmo(int D, const ReduceFrame* frames, int nframes, const float* X, float* C,
-                                       float* fs, int* is, uint32_t* /*bits*/, hipStream_t st) {
+                                       float* fs, int* is, uint32_t* /*bits*/, int max_n, hipStream_t st) {
     dim3 grid(nframes), block(kYThreads);
+    const size_t shm = yakmo_dyn_lds(max_n);
+    hipError_t e = hipSuccess;
     switch (D) {
-    case 8: hipLaunchKernelGGL(yakmo_seed2_kernel<8>, grid, block, 0, st, frames, nframes, X, C, fs, is); break;
-    case 16: hipLaunchKernelGGL(yakmo_seed2_kernel<16>, grid, block, 0, st, frames, nframes, X, C, fs, is); break;
-    case 32: hipLaunchKernelGGL(yakmo_seed2_kernel<32>, grid, block, 0, st, frames, nframes, X, C, fs, is); break;
+#define YK(DV)                                                                                                  \
+    case DV:                                                                                                    \
+        e = hipFuncSetAttribute((const void*)yakmo_seed2_kernel<DV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                (int)shm);                                                                      \
+        if (e != hipSuccess) return e;                                                                          \
+        hipLaunchKernelGGL(yakmo_seed2_kernel<DV>, grid, block, shm, st, frames, nframes, X, C, fs, is);         \
+        break;
+        YK(8)
+        YK(16)
+        YK(32)
+#undef YK
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
