@@ -28,10 +28,17 @@ __device__ __forceinline__ int64_t ceil_pos_d(double x) {  // FPC math.ceil, x >
 
 // FindAttenuationDivider: lane = candidate law 1/(lane+1); each lane runs the
 // reference's sequential f64 error sum over (channel, chunk, sample), then the
-// first lane at the minimum wins (strict <, laws in order).
+// first lane at the minimum wins (strict <, laws in order).  One wave per
+// frame: the samples are staged through LDS in 1024-sample batches, the next
+// batch's coalesced loads in flight while the current one is summed (a load
+// per chunk waited out the HBM latency on every chunk: 62 ms for 256 frames).
+constexpr int kAttBatch = 1024;  // samples per staged batch (16 per lane)
+
 template <int CS>
 __global__ __launch_bounds__(64) void atten_kernel(DspFrame* __restrict__ frames, int nframes,
                                                    const double* __restrict__ samp, int64_t span, int ch, int obd) {
+    static_assert(kAttBatch % CS == 0, "whole chunks per batch");
+    __shared__ double buf[kAttBatch];
     const int fi = blockIdx.x;
     if (fi >= nframes) return;
     DspFrame* fr = frames + fi;
@@ -48,44 +55,66 @@ __global__ __launch_bounds__(64) void atten_kernel(DspFrame* __restrict__ frames
         }
     }
     const int sc = fr->sc, nck = sc / CS;
+    const int tot = nck * CS;  // samples of whole chunks per channel
     const double dobd = double(obd);
     double v = 0.0;
+    constexpr int kPer = kAttBatch / 64;
     for (int j = 0; j < ch; ++j) {
         const double* src = samp + int64_t(j) * span + fr->s_off;
-        for (int k = 0; k < nck; ++k) {
-            double x[CS];
+        double nx[kPer];
 #pragma unroll
-            for (int l = 0; l < CS; ++l) x[l] = src[k * CS + l];
-            // hiSmp (encoder.lpr:1687-1689)
-            int64_t hi = 0;
+        for (int e = 0; e < kPer; ++e) {
+            const int t = e * 64 + lane;
+            nx[e] = t < tot ? src[t] : 0.0;
+        }
+        for (int t0 = 0; t0 < tot; t0 += kAttBatch) {
+            __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (int l = 0; l < CS; ++l) {
-                const int64_t h = ceil_pos_d(fabs(x[l] * 32767.0));
-                hi = h > hi ? h : hi;
+            for (int e = 0; e < kPer; ++e) buf[e * 64 + lane] = nx[e];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+#pragma unroll
+            for (int e = 0; e < kPer; ++e) {  // the next batch's loads
+                const int t = t0 + kAttBatch + e * 64 + lane;
+                nx[e] = t < tot ? src[t] : 0.0;
             }
-            // ComputeAttenuation (encoder.lpr:1691-1697): coeff after r steps = coeff[r]
-            int a = kMaxAtt;
-            for (int r = 1; r <= kMaxAtt; ++r)
-                if (double(hi) * coeff[r] > 32767.0) {
-                    a = r - 1;
-                    break;
+            const int kn = min(kAttBatch, tot - t0) / CS;
+            for (int k = 0; k < kn; ++k) {
+                double x[CS];
+#pragma unroll
+                for (int l = 0; l < CS; ++l) x[l] = buf[k * CS + l];
+                // hiSmp (encoder.lpr:1687-1689)
+                int64_t hi = 0;
+#pragma unroll
+                for (int l = 0; l < CS; ++l) {
+                    const int64_t h = ceil_pos_d(fabs(x[l] * 32767.0));
+                    hi = h > hi ? h : hi;
                 }
-            double cf = coeff[0];
+                // ComputeAttenuation (encoder.lpr:1691-1697): coeff after r steps = coeff[r]
+                int a = kMaxAtt;
+                for (int r = 1; r <= kMaxAtt; ++r)
+                    if (double(hi) * coeff[r] > 32767.0) {
+                        a = r - 1;
+                        break;
+                    }
+                double cf = coeff[0];
 #pragma unroll
-            for (int q = 1; q <= kMaxAtt; ++q) cf = q == a ? coeff[q] : cf;
-            const double den = dobd * cf;
+                for (int q = 1; q <= kMaxAtt; ++q) cf = q == a ? coeff[q] : cf;
+                const double den = dobd * cf;
 #pragma unroll
-            for (int l = 0; l < CS; ++l) {
-                // makeOutputSample (encoder.lpr:1648-1663): Round, SmallInt wrap, clamp
-                int s16 = (int)(int16_t)(int64_t)rint(x[l] * dobd * cf);
-                s16 = max(s16, -obd + 1);
-                s16 = min(s16, obd - 1);
-                // makeFloatSample (encoder.lpr:1665-1680)
-                double r = double(s16) / den;
-                r = r < -1.0 ? -1.0 : r;
-                r = r > 1.0 ? 1.0 : r;
-                const double dd = x[l] - r;
-                v += dd * dd;
+                for (int l = 0; l < CS; ++l) {
+                    // makeOutputSample (encoder.lpr:1648-1663): Round, SmallInt wrap, clamp
+                    int s16 = (int)(int16_t)(int64_t)rint(x[l] * dobd * cf);
+                    s16 = max(s16, -obd + 1);
+                    s16 = min(s16, obd - 1);
+                    // makeFloatSample (encoder.lpr:1665-1680)
+                    double r = double(s16) / den;
+                    r = r < -1.0 ? -1.0 : r;
+                    r = r > 1.0 ? 1.0 : r;
+                    const double dd = x[l] - r;
+                    v += dd * dd;
+                }
             }
         }
     }

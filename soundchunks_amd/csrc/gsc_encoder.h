@@ -2,10 +2,13 @@
 // of reference encoder/encoder.lpr around the GPU hot path.
 //
 //   host  : Load + PrepareFrames (encoder.lpr:1111-1152, 1294-1429),
-//           FindAttenuationDivider (566-605), MakeChunks features (349-485),
-//           cluster means + FPC QuickSort (843-889), KNNFit pruning/sort
-//           (970-977), SaveStream bit packing (980-1107)
-//   device: yakmo seeding, KNNScanReduce, KNNFit search (gsc_kernels.hip)
+//           cluster means + FPC QuickSort (843-889), KNNFit pruning/sort by
+//           use count (970-977), SaveStream header and codebook (980-1048)
+//   device: FindAttenuationDivider (566-605) and the MakeChunks features
+//           (349-485, gsc_dsp.hip), yakmo seeding (gsc_yakmo.hip),
+//           KNNScanReduce (gsc_scan.hip), KNNFit search (gsc_kernels.hip),
+//           use counts and the SaveStream index bitstream (1050-1106,
+//           gsc_pack.hip), reconstruction (gsc_recon.hip)
 #pragma once
 #include <cstdint>
 #include <functional>

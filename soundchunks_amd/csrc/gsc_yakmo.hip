@@ -10,7 +10,7 @@
 // lower_bound searches.  That prefix is one sequential f32 chain per pick.
 //
 // Roles: wave 0 picks and chains; waves 1..8 compute one 512-point block per
-// step (one point per thread), d0 and seed ids prefetched eight steps ahead and
+// step (one point per thread), d0 and seed ids prefetched four steps ahead and
 // the X rows of points that the Elkan bound cannot skip two steps ahead.
 // The chain turns each run of whole 64-point blocks into one integer prefix
 // sum while the total stays in one binade (chain_fast: exact, or the blocks
@@ -40,7 +40,7 @@ __device__ __forceinline__ bool yakmo_idle_wave(int w) { return w == 4 || w == 8
 // distance thread index of a distance wave's lane
 __device__ __forceinline__ int yakmo_dist_index(int w, int lane) { return (w - 1 - w / 4) * 64 + lane; }
 constexpr int kYBits = 262144 / 32;   // chosen-point bitmap in LDS (N <= 262144)
-constexpr int kYPre = 8;              // d0 / seed-id prefetch depth (steps); X rows: 2
+constexpr int kYPre = 4;              // d0 / seed-id prefetch depth (steps); X rows: 2
 
 #ifdef GSC_STAMPS
 // diagnostic phase clocks (make stamps): s_memtime deltas per role
@@ -499,7 +499,7 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
                 return sh.sdlo[a] >= need;
             };
             // pipeline: step b computes block b; the X rows of block b + XD (when
-            // not skipped) and the d0 / seed ids of block b + 8 are loaded meanwhile
+            // not skipped) and the d0 / seed ids of block b + 4 are loaded meanwhile
             constexpr int XD = D == 32 ? 1 : 2;  // X-row look-ahead (VGPR budget of 9 waves)
             float xv[XD][D];
             bool skip[XD];
