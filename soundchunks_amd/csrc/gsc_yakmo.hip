@@ -9,9 +9,11 @@
 // <) and, for i < K-1, the running f32 total cum[n] that the next pick's
 // lower_bound searches.  That prefix is one sequential f32 chain per pick.
 //
-// Roles: wave 0 picks and chains; waves 1..8 compute one 512-point block per
-// step (one point per thread), d0 and seed ids prefetched four steps ahead and
-// the X rows of points that the Elkan bound cannot skip two steps ahead.
+// Roles: wave 0 picks and chains; 8 distance waves compute one 1024-point
+// block per step (two points per thread; 512 at D = 32), d0 and seed ids
+// prefetched three steps ahead and the X rows of points that the Elkan bound
+// cannot skip one step ahead; three more waves only keep the barriers, so the
+// chain issues alone on its SIMD.
 // The chain turns each run of whole 64-point blocks into one integer prefix
 // sum while the total stays in one binade (chain_fast: exact, or the blocks
 // are added one by one), and keeps per 64-point block the checkpoint cum and
@@ -32,7 +34,13 @@ __device__ __forceinline__ float fs(float a, float b) { return __fsub_rn(a, b); 
 __device__ __forceinline__ float fm(float a, float b) { return __fmul_rn(a, b); }
 
 constexpr int kYDist = 512;            // distance threads (8 waves)
-constexpr int kYBlock = kYDist;        // points per pipeline step: one per distance thread
+// points per distance thread per step (kYDist apart): two at D <= 16, one at
+// D = 32 (VGPR budget)
+template <int D>
+constexpr int yakmo_pts() {
+    return D == 32 ? 1 : 2;
+}
+constexpr int kYBlock = kYDist * 2;    // ring capacity: points per step (largest)
 // 12 waves, 3 per SIMD: wave 0 picks and chains; waves 4, 8 and 11 only keep
 // the barriers, so SIMD 0 issues the chain alone; the other 8 compute distances
 constexpr int kYThreads = 768;
@@ -40,7 +48,7 @@ __device__ __forceinline__ bool yakmo_idle_wave(int w) { return w == 4 || w == 8
 // distance thread index of a distance wave's lane
 __device__ __forceinline__ int yakmo_dist_index(int w, int lane) { return (w - 1 - w / 4) * 64 + lane; }
 constexpr int kYBits = 262144 / 32;   // chosen-point bitmap in LDS (N <= 262144)
-constexpr int kYPre = 4;              // d0 / seed-id prefetch depth (steps); X rows: 2
+constexpr int kYPre = 3;              // d0 / seed-id prefetch depth (steps); X rows: 1
 
 #ifdef GSC_STAMPS
 // diagnostic phase clocks (make stamps): s_memtime deltas per role
@@ -150,46 +158,52 @@ __device__ __forceinline__ uint32_t oct_max_u32(uint32_t v) {
 // those conditions the chain is an integer prefix sum: the d/u roundings are
 // independent of each other and of the order, and the integer sums are exact.
 //
-// Points s .. s + 64 nbk - 1 of the ring (nbk <= 8 blocks, s a multiple of
-// 64); lane l takes 8 consecutive points: one local prefix, one wave scan.
-// The blocks before the first point that breaks a condition (tie, |d/u| >=
-// 2^24, a partial out of range) are accepted: their checkpoints and min/max
-// are written (global block index g0 + k) and *run_io moves to the last
-// accepted partial.  Returns the accepted block count.  run must be at least
-// 2^-100, so that 2^sc is a normal f32 and d * 2^sc is exact wherever it
-// matters (a d/u far below 1/2 may round: it still rounds to 0, no tie).
+// Points s .. s + 64 nbk - 1 of the ring (nbk <= 64 PPL / 64 blocks, s a
+// multiple of 64); lane l takes PPL consecutive points: one local prefix, one
+// wave scan.  The blocks before the first point that breaks a condition (tie,
+// |d/u| >= 2^24, a partial out of range) are accepted: their checkpoints and
+// min/max are written (global block index g0 + k) and *run_io moves to the
+// last accepted partial.  Returns the accepted block count.  run must be at
+// least 2^-100, so that 2^sc is a normal f32 and d * 2^sc is exact wherever
+// it matters (a d/u far below 1/2 may round: it still rounds to 0, no tie).
+template <int PPL>
 __device__ __forceinline__ int chain_fast(const float* __restrict__ ring, int s, int nbk, int lane, float* run_io,
                                           float* ck, float* bmn, float* bmx, int g0) {
+    static_assert(PPL == 8 || PPL == 16, "8 or 16 points per lane");
+    constexpr int LPB = 64 / PPL;  // lanes per 64-point block
     const float run = *run_io;
     if (!(run >= 7.88860905e-31f)) return 0;  // below 2^-100, zero, negative (or NaN)
     const int fe = __builtin_amdgcn_frexp_expf(run);  // run = f * 2^fe, f in [0.5, 1)
     const int sc = 24 - fe;                          // d/u = d * 2^sc, sc <= 124
     const float scale = __builtin_ldexpf(1.0f, sc), unscale = __builtin_ldexpf(1.0f, -sc);
     const uint32_t m0 = (uint32_t)(run * scale);  // in [2^23, 2^24), exact
-    const bool act = lane < nbk * 8;
-    float v[8];
+    const bool act = lane < nbk * LPB;
+    float v[PPL];
     if (act) {
-        const float4 a = *reinterpret_cast<const float4*>(&ring[s + 8 * lane]);
-        const float4 b = *reinterpret_cast<const float4*>(&ring[s + 8 * lane + 4]);
-        v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
+#pragma unroll
+        for (int h = 0; h < PPL / 4; ++h) {
+            const float4 a = *reinterpret_cast<const float4*>(&ring[s + PPL * lane + 4 * h]);
+            v[4 * h] = a.x, v[4 * h + 1] = a.y, v[4 * h + 2] = a.z, v[4 * h + 3] = a.w;
+        }
     } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = 0.0f;
+        for (int e = 0; e < PPL; ++e) v[e] = 0.0f;
     }
-    uint32_t q[8], acc = 0;
-    bool ok[8];
+    uint32_t q[PPL], acc = 0;
+    bool ok[PPL];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
+    for (int e = 0; e < PPL; ++e) {
         const float t = v[e] * scale;
         const float n = __builtin_rintf(t);
         ok[e] = __builtin_fabsf(t) < 16777216.0f && __builtin_fabsf(t - n) != 0.5f;  // NaN: not ok
         acc += (uint32_t)(int)n;  // garbage where !ok: that point fails below anyway
         q[e] = acc;
     }
+    // (a uint32 wrap needs an earlier partial out of range, which fails first)
     const uint32_t base = m0 + (wave_scan_u32(acc) - acc);
-    uint64_t bad[8], anyb = 0;
+    uint64_t bad[PPL], anyb = 0;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
+    for (int e = 0; e < PPL; ++e) {
         q[e] += base;
         // m + partial in [2^23 + 1, 2^24 - 2]: the exact sum, within 1/2 of
         // it, lies strictly inside the binade and rounds on the grid u
@@ -199,30 +213,38 @@ __device__ __forceinline__ int chain_fast(const float* __restrict__ ring, int s,
     int k = nbk;
     if (anyb) {
         const int L = __builtin_ctzll(anyb);
-        int e0 = 7;
+        int e0 = PPL - 1;
 #pragma unroll
-        for (int e = 7; e >= 0; --e)
+        for (int e = PPL - 1; e >= 0; --e)
             if ((bad[e] >> L) & 1ull) e0 = e;
-        k = min(nbk, (L * 8 + e0) >> 6);
+        k = min(nbk, (L * PPL + e0) >> 6);
     }
     if (k == 0) return 0;
     uint32_t mn = q[0], mx = q[0];
 #pragma unroll
-    for (int e = 1; e < 8; ++e) {
+    for (int e = 1; e < PPL; ++e) {
         mn = min(mn, q[e]);
         mx = max(mx, q[e]);
     }
-    mn = oct_min_u32(mn);  // in range, so integer order is the partials' order
-    mx = oct_max_u32(mx);
-    const int blk = lane >> 3;
+    // in range, so integer order is the partials' order
+    if constexpr (PPL == 8) {
+        mn = oct_min_u32(mn);
+        mx = oct_max_u32(mx);
+    } else {
+        mn = min(mn, (uint32_t)__builtin_amdgcn_mov_dpp((int)mn, 0xb1, 0xf, 0xf, false));
+        mx = max(mx, (uint32_t)__builtin_amdgcn_mov_dpp((int)mx, 0xb1, 0xf, 0xf, false));
+        mn = min(mn, (uint32_t)__builtin_amdgcn_mov_dpp((int)mn, 0x4e, 0xf, 0xf, false));
+        mx = max(mx, (uint32_t)__builtin_amdgcn_mov_dpp((int)mx, 0x4e, 0xf, 0xf, false));
+    }
+    const int blk = lane / LPB;
     if (blk < k) {
-        if ((lane & 7) == 0) {
+        if ((lane % LPB) == 0) {
             bmn[g0 + blk] = (float)mn * unscale;  // exact: < 2^24, same binade
             bmx[g0 + blk] = (float)mx * unscale;
         }
-        if ((lane & 7) == 7) ck[g0 + blk] = (float)q[7] * unscale;
+        if ((lane % LPB) == LPB - 1) ck[g0 + blk] = (float)q[PPL - 1] * unscale;
     }
-    *run_io = (float)(uint32_t)__builtin_amdgcn_readlane((int)q[7], 8 * k - 1) * unscale;
+    *run_io = (float)(uint32_t)__builtin_amdgcn_readlane((int)q[PPL - 1], LPB * k - 1) * unscale;
     return k;
 }
 
@@ -379,7 +401,8 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
 
     uint64_t rx = 123456789ull, ry = 362436069ull, rz = 521288629ull, rw = 88675123ull;
     float total = 0.0f;
-    constexpr int BLK = kYBlock;
+    constexpr int kYPts = yakmo_pts<D>();
+    constexpr int BLK = kYDist * kYPts;  // points per pipeline step
     const int nblk = (N + BLK - 1) / BLK;
     const bool idle = yakmo_idle_wave(wave);
     const int dt = (wave == 0 || idle) ? -1 : yakmo_dist_index(wave, lane);  // distance thread index
@@ -393,19 +416,21 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
         rw = rw ^ (rw >> 19) ^ t ^ (t >> 8);
         const float r = (float)((double)rw * 5.42101086242752217e-20);  // f32(f64(w) * 2^-64)
         // distance waves: this pick's first seed ids / d0 are in flight during the pick
-        float pd[kYPre];
-        int pa[kYPre];
+        float pd[kYPre][kYPts];
+        int pa[kYPre][kYPts];
         if (dt >= 0) {
 #pragma unroll
-            for (int q = 0; q < kYPre; ++q) {
-                const int n = q * BLK + dt;
-                pd[q] = 0.0f;
-                pa[q] = 0;
-                if (i > 0 && n < N) {
-                    pd[q] = d0[n];
-                    pa[q] = id16[n];
+            for (int q = 0; q < kYPre; ++q)
+#pragma unroll
+                for (int p = 0; p < kYPts; ++p) {
+                    const int n = q * BLK + p * kYDist + dt;
+                    pd[q][p] = 0.0f;
+                    pa[q][p] = 0;
+                    if (i > 0 && n < N) {
+                        pd[q][p] = d0[n];
+                        pa[q][p] = id16[n];
+                    }
                 }
-            }
         }
         if (wave == 0) {
             uint32_t idx;
@@ -448,7 +473,7 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
                     while (s < cnt) {
                         const int full = (cnt - s) >> 6;
                         if (full > 0) {
-                            const int k = chain_fast(rg, s, full, lane, &run, ck, bmn, bmx, (base + s) >> 6);
+                            const int k = chain_fast<BLK / 64>(rg, s, full, lane, &run, ck, bmn, bmx, (base + s) >> 6);
                             s += k << 6;
                             YST(1) YCNT(4)
                             if (s >= cnt) break;
@@ -498,63 +523,73 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
                 const float need = fm(fm(fa(fmaxf(dold, 0.0f), e), 4.0f), 1.00000381f);
                 return sh.sdlo[a] >= need;
             };
-            // pipeline: step b computes block b; the X rows of block b + XD (when
-            // not skipped) and the d0 / seed ids of block b + 4 are loaded meanwhile
-            constexpr int XD = D == 32 ? 1 : 2;  // X-row look-ahead (VGPR budget of 9 waves)
-            float xv[XD][D];
-            bool skip[XD];
+            // pipeline: step b computes block b (kYPts points per thread, kYDist
+            // apart); the X rows of block b + XD (when not skipped) and the d0 /
+            // seed ids of block b + kYPre are loaded meanwhile
+            constexpr int XD = 1;  // X-row look-ahead in steps (a step is 1024 points)
+            float xv[XD][kYPts][D];
+            bool skip[XD][kYPts];
 #pragma unroll
-            for (int q = 0; q < XD; ++q) {
-                const int n = q * BLK + dt;
-                skip[q] = true;
-                if (n < N) {
-                    skip[q] = skip_of(pd[q], pa[q]);
-                    if (!skip[q]) {
+            for (int q = 0; q < XD; ++q)
 #pragma unroll
-                        for (int j = 0; j < D; ++j) xv[q][j] = X[(int64_t)n * D + j];
+                for (int p = 0; p < kYPts; ++p) {
+                    const int n = q * BLK + p * kYDist + dt;
+                    skip[q][p] = true;
+                    if (n < N) {
+                        skip[q][p] = skip_of(pd[q][p], pa[q][p]);
+                        if (!skip[q][p]) {
+#pragma unroll
+                            for (int j = 0; j < D; ++j) xv[q][p][j] = X[(int64_t)n * D + j];
+                        }
                     }
                 }
-            }
             for (int b0 = 0; b0 <= nblk; b0 += kYPre) {
 #pragma unroll
                 for (int u = 0; u < kYPre; ++u) {
                     const int b = b0 + u;
                     if (b > nblk) break;
                     const int s2 = u % XD;
-                    const int n = b * BLK + dt;
-                    if (b < nblk && n < N) {
-                        float dn = pd[u];
-                        if (!skip[s2]) {
-                            float xn = 0.0f;  // yakmo's |x|^2, as computed at the start
 #pragma unroll
-                            for (int j = 0; j < D; ++j) xn = fa(xn, fm(xv[s2][j], xv[s2][j]));
-                            float d = fa(fa(cn, xn), 0.0f);
+                    for (int p = 0; p < kYPts; ++p) {
+                        const int n = b * BLK + p * kYDist + dt;
+                        if (b < nblk && n < N) {
+                            float dn = pd[u][p];
+                            if (!skip[s2][p]) {
+                                float xn = 0.0f;  // yakmo's |x|^2, as computed at the start
 #pragma unroll
-                            for (int j = 0; j < D; ++j) d = fs(d, fm(fa(xv[s2][j], xv[s2][j]), c[j]));
-                            if (i == 0 || dn > d) {
-                                dn = d;
-                                d0[n] = d;
-                                idv[n] = i;
-                                id16[n] = (uint16_t)i;
+                                for (int j = 0; j < D; ++j) xn = fa(xn, fm(xv[s2][p][j], xv[s2][p][j]));
+                                float d = fa(fa(cn, xn), 0.0f);
+#pragma unroll
+                                for (int j = 0; j < D; ++j) d = fs(d, fm(fa(xv[s2][p][j], xv[s2][p][j]), c[j]));
+                                if (i == 0 || dn > d) {
+                                    dn = d;
+                                    d0[n] = d;
+                                    idv[n] = i;
+                                    id16[n] = (uint16_t)i;
+                                }
+                            }
+                            sh.ring[b & 1][p * kYDist + dt] = dn;
+                        }
+                    }
+#pragma unroll
+                    for (int p = 0; p < kYPts; ++p) {
+                        const int n = b * BLK + p * kYDist + dt;
+                        // block b + XD: skip decision and X rows (slot s2 is free now)
+                        const int n2 = n + XD * BLK;
+                        skip[s2][p] = true;
+                        if (b + XD < nblk && n2 < N) {
+                            skip[s2][p] = skip_of(pd[(u + XD) % kYPre][p], pa[(u + XD) % kYPre][p]);
+                            if (!skip[s2][p]) {
+#pragma unroll
+                                for (int j = 0; j < D; ++j) xv[s2][p][j] = X[(int64_t)n2 * D + j];
                             }
                         }
-                        sh.ring[b & 1][dt] = dn;
-                    }
-                    // block b + XD: skip decision and X rows (slot s2 is free now)
-                    const int n2 = n + XD * BLK;
-                    skip[s2] = true;
-                    if (b + XD < nblk && n2 < N) {
-                        skip[s2] = skip_of(pd[(u + XD) % kYPre], pa[(u + XD) % kYPre]);
-                        if (!skip[s2]) {
-#pragma unroll
-                            for (int j = 0; j < D; ++j) xv[s2][j] = X[(int64_t)n2 * D + j];
+                        // block b + kYPre: d0 and seed id (slot u is free now)
+                        const int n4 = n + kYPre * BLK;
+                        if (i > 0 && b + kYPre < nblk && n4 < N) {
+                            pd[u][p] = d0[n4];
+                            pa[u][p] = id16[n4];
                         }
-                    }
-                    // block b + kYPre: d0 and seed id (slot u is free now)
-                    const int n4 = n + kYPre * BLK;
-                    if (i > 0 && b + kYPre < nblk && n4 < N) {
-                        pd[u] = d0[n4];
-                        pa[u] = id16[n4];
                     }
                     YST(9)
                     step_barrier(b == nblk);
