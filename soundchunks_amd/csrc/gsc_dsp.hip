@@ -26,6 +26,14 @@ __device__ __forceinline__ int64_t ceil_pos_d(double x) {  // FPC math.ceil, x >
     return r;
 }
 
+// the same for 0 <= x < 2^31 with the native f64 -> i32 conversion
+__device__ __forceinline__ int ceil_pos_i32(double x) {
+    const double t = trunc(x);
+    int r = (int)t;
+    if (x - t > 0.0) ++r;
+    return r;
+}
+
 // FindAttenuationDivider: lane = candidate law 1/(lane+1); each lane runs the
 // reference's sequential f64 error sum over (channel, chunk, sample), then the
 // first lane at the minimum wins (strict <, laws in order).  One wave per
@@ -84,11 +92,12 @@ __global__ __launch_bounds__(64) void atten_kernel(DspFrame* __restrict__ frames
                 double x[CS];
 #pragma unroll
                 for (int l = 0; l < CS; ++l) x[l] = buf[k * CS + l];
-                // hiSmp (encoder.lpr:1687-1689)
-                int64_t hi = 0;
+                // hiSmp (encoder.lpr:1687-1689); |x| <= 32768/32767, so every value
+                // here fits an int32 and the native conversions are exact
+                int hi = 0;
 #pragma unroll
                 for (int l = 0; l < CS; ++l) {
-                    const int64_t h = ceil_pos_d(fabs(x[l] * 32767.0));
+                    const int h = ceil_pos_i32(fabs(x[l] * 32767.0));
                     hi = h > hi ? h : hi;
                 }
                 // ComputeAttenuation (encoder.lpr:1691-1697): coeff after r steps = coeff[r]
@@ -105,7 +114,8 @@ __global__ __launch_bounds__(64) void atten_kernel(DspFrame* __restrict__ frames
 #pragma unroll
                 for (int l = 0; l < CS; ++l) {
                     // makeOutputSample (encoder.lpr:1648-1663): Round, SmallInt wrap, clamp
-                    int s16 = (int)(int16_t)(int64_t)rint(x[l] * dobd * cf);
+                    // (|x obd cf| <= 1.00003 * 32767 * 121 < 2^22: the i32 conversion is exact)
+                    int s16 = (int)(int16_t)(int)rint(x[l] * dobd * cf);
                     s16 = max(s16, -obd + 1);
                     s16 = min(s16, obd - 1);
                     // makeFloatSample (encoder.lpr:1665-1680)

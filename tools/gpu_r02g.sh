@@ -12,3 +12,5 @@ grep -E "host timing" gpurun_out/bench_g.log | tail -2
 tail -1 gpurun_out/bench_g.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['realtime_x'], d['ms_per_step'], d['stages_ms'], d['roofline']['frac'])"
 GSC_LIB=soundchunks_amd/lib/stamps/libsoundchunks_amd.so GSC_HOST_TIMING=1 timeout -k 10 300 python -u bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/bench_stamps_g.log 2>&1 || { tail -20 gpurun_out/bench_stamps_g.log; exit 4; }
 grep -E "yakmo stamps" gpurun_out/bench_stamps_g.log
+GSC_LIB=soundchunks_amd/lib/var8/libsoundchunks_amd.so GSC_HOST_TIMING=1 timeout -k 10 300 python -u bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/bench_var8.log 2>&1 || { tail -20 gpurun_out/bench_var8.log; exit 5; }
+echo "var8:"; grep -E "host timing" gpurun_out/bench_var8.log | tail -1
