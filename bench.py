@@ -226,6 +226,9 @@ def main():
                                                     "gpu_scan_ms", "gpu_knnfit_ms", "host_post_ms", "post_overlap_ms",
                                                     "total_ms")},
         "post_groups": tm["post_groups"],
+        "stages_note": ("host_frames, gpu_dsp, gpu_yakmo, gpu_scan and host_post run in series; gpu_knnfit_ms is "
+                        "submit-to-done of the KNNFit groups, which run on the CUs of finished frames during the "
+                        "scan tail (post_overlap_ms), so it is not additive"),
         "scan": {"passes": tm["scan_passes"], "searches": tm["scan_point_passes"], "exact_dfs": tm["scan_slow"],
                  "solo_resolutions": tm["scan_restarts"]},
     }
