@@ -36,21 +36,29 @@ __device__ __forceinline__ int ceil_pos_i32(double x) {
 
 // FindAttenuationDivider: lane = candidate law 1/(lane+1); each lane runs the
 // reference's sequential f64 error sum over (channel, chunk, sample), then the
-// first lane at the minimum wins (strict <, laws in order).  One wave per
-// frame: the samples are staged through LDS in 1024-sample batches, the next
-// batch's coalesced loads in flight while the current one is summed (a load
-// per chunk waited out the HBM latency on every chunk: 62 ms for 256 frames).
-constexpr int kAttBatch = 1024;  // samples per staged batch (16 per lane)
+// first lane at the minimum wins (strict <, laws in order).
+//
+// One workgroup of 8 waves per frame.  The error terms (x - r)^2 of a batch
+// of kAttBatch samples are independent across samples: seven producer waves
+// compute them (chunk c of the batch on wave 1 + c % 7, lane = law) into LDS,
+// and wave 0 adds them in the reference's order while the producers fill the
+// other buffer.  Every term is the reference's own arithmetic, and the sum is
+// the same sequential chain, so the result is unchanged; the f64 latency
+// chains now run on all four SIMDs instead of one.
+constexpr int kAttProd = 7;                  // producer waves
+constexpr int kAttBatch = kAttProd * 16;     // samples per batch: whole chunks for CS = 4, 8, 16
+constexpr int kAttThreads = 64 * (kAttProd + 1);
 
 template <int CS>
-__global__ __launch_bounds__(64) void atten_kernel(DspFrame* __restrict__ frames, int nframes,
-                                                   const double* __restrict__ samp, int64_t span, int ch, int obd) {
-    static_assert(kAttBatch % CS == 0, "whole chunks per batch");
-    __shared__ double buf[kAttBatch];
+__global__ __launch_bounds__(kAttThreads) void atten_kernel(DspFrame* __restrict__ frames, int nframes,
+                                                            const double* __restrict__ samp, int64_t span, int ch,
+                                                            int obd) {
+    static_assert(kAttBatch % (CS * kAttProd) == 0, "whole chunks per producer");
+    extern __shared__ __attribute__((aligned(16))) double aterm[];  // [2][kAttBatch][64]
     const int fi = blockIdx.x;
     if (fi >= nframes) return;
     DspFrame* fr = frames + fi;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const double law = 1.0 / double(lane + 1);
     // coeff(a) = 1 + sum_{i=0..a} i*law, left to right (encoder.lpr:1654-1656)
     double coeff[kMaxAtt + 1];
@@ -64,70 +72,66 @@ __global__ __launch_bounds__(64) void atten_kernel(DspFrame* __restrict__ frames
     }
     const int sc = fr->sc, nck = sc / CS;
     const int tot = nck * CS;  // samples of whole chunks per channel
+    const int nbat = (tot + kAttBatch - 1) / kAttBatch;
     const double dobd = double(obd);
     double v = 0.0;
-    constexpr int kPer = kAttBatch / 64;
     for (int j = 0; j < ch; ++j) {
         const double* src = samp + int64_t(j) * span + fr->s_off;
-        double nx[kPer];
+        for (int t = 0; t <= nbat; ++t) {
+            if (wave > 0 && t < nbat) {
+                // terms of batch t into buffer t & 1
+                double* T = aterm + size_t(t & 1) * kAttBatch * 64;
+                const int t0 = t * kAttBatch;
+                const int kn = min(kAttBatch, tot - t0) / CS;
+                for (int k = wave - 1; k < kn; k += kAttProd) {
+                    double x[CS];
 #pragma unroll
-        for (int e = 0; e < kPer; ++e) {
-            const int t = e * 64 + lane;
-            nx[e] = t < tot ? src[t] : 0.0;
-        }
-        for (int t0 = 0; t0 < tot; t0 += kAttBatch) {
-            __builtin_amdgcn_wave_barrier();
+                    for (int l = 0; l < CS; ++l) x[l] = src[t0 + k * CS + l];
+                    // hiSmp (encoder.lpr:1687-1689); |x| <= 32768/32767, so every value
+                    // here fits an int32 and the native conversions are exact
+                    int hi = 0;
 #pragma unroll
-            for (int e = 0; e < kPer; ++e) buf[e * 64 + lane] = nx[e];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-#pragma unroll
-            for (int e = 0; e < kPer; ++e) {  // the next batch's loads
-                const int t = t0 + kAttBatch + e * 64 + lane;
-                nx[e] = t < tot ? src[t] : 0.0;
-            }
-            const int kn = min(kAttBatch, tot - t0) / CS;
-            for (int k = 0; k < kn; ++k) {
-                double x[CS];
-#pragma unroll
-                for (int l = 0; l < CS; ++l) x[l] = buf[k * CS + l];
-                // hiSmp (encoder.lpr:1687-1689); |x| <= 32768/32767, so every value
-                // here fits an int32 and the native conversions are exact
-                int hi = 0;
-#pragma unroll
-                for (int l = 0; l < CS; ++l) {
-                    const int h = ceil_pos_i32(fabs(x[l] * 32767.0));
-                    hi = h > hi ? h : hi;
-                }
-                // ComputeAttenuation (encoder.lpr:1691-1697): coeff after r steps = coeff[r]
-                int a = kMaxAtt;
-                for (int r = 1; r <= kMaxAtt; ++r)
-                    if (double(hi) * coeff[r] > 32767.0) {
-                        a = r - 1;
-                        break;
+                    for (int l = 0; l < CS; ++l) {
+                        const int h = ceil_pos_i32(fabs(x[l] * 32767.0));
+                        hi = h > hi ? h : hi;
                     }
-                double cf = coeff[0];
+                    // ComputeAttenuation (encoder.lpr:1691-1697): coeff after r steps = coeff[r]
+                    int a = kMaxAtt;
+                    for (int r = 1; r <= kMaxAtt; ++r)
+                        if (double(hi) * coeff[r] > 32767.0) {
+                            a = r - 1;
+                            break;
+                        }
+                    double cf = coeff[0];
 #pragma unroll
-                for (int q = 1; q <= kMaxAtt; ++q) cf = q == a ? coeff[q] : cf;
-                const double den = dobd * cf;
+                    for (int q = 1; q <= kMaxAtt; ++q) cf = q == a ? coeff[q] : cf;
+                    const double den = dobd * cf;
 #pragma unroll
-                for (int l = 0; l < CS; ++l) {
-                    // makeOutputSample (encoder.lpr:1648-1663): Round, SmallInt wrap, clamp
-                    // (|x obd cf| <= 1.00003 * 32767 * 121 < 2^22: the i32 conversion is exact)
-                    int s16 = (int)(int16_t)(int)rint(x[l] * dobd * cf);
-                    s16 = max(s16, -obd + 1);
-                    s16 = min(s16, obd - 1);
-                    // makeFloatSample (encoder.lpr:1665-1680)
-                    double r = double(s16) / den;
-                    r = r < -1.0 ? -1.0 : r;
-                    r = r > 1.0 ? 1.0 : r;
-                    const double dd = x[l] - r;
-                    v += dd * dd;
+                    for (int l = 0; l < CS; ++l) {
+                        // makeOutputSample (encoder.lpr:1648-1663): Round, SmallInt wrap, clamp
+                        // (|x obd cf| <= 1.00003 * 32767 * 121 < 2^22: the i32 conversion is exact)
+                        int s16 = (int)(int16_t)(int)rint(x[l] * dobd * cf);
+                        s16 = max(s16, -obd + 1);
+                        s16 = min(s16, obd - 1);
+                        // makeFloatSample (encoder.lpr:1665-1680)
+                        double r = double(s16) / den;
+                        r = r < -1.0 ? -1.0 : r;
+                        r = r > 1.0 ? 1.0 : r;
+                        const double dd = x[l] - r;
+                        T[(k * CS + l) * 64 + lane] = dd * dd;
+                    }
                 }
             }
+            if (wave == 0 && t > 0) {
+                // the reference's sum over batch t - 1, in sample order
+                const double* T = aterm + size_t((t - 1) & 1) * kAttBatch * 64;
+                const int n = min(kAttBatch, tot - (t - 1) * kAttBatch);
+                for (int q = 0; q < n; ++q) v += T[q * 64 + lane];
+            }
+            __syncthreads();
         }
     }
+    if (wave != 0) return;
     // first lane at the minimum (best starts at MaxSingle, v < best)
     double best = v;
     int bi = lane;
@@ -264,13 +268,23 @@ extern "C" hipError_t gsc_launch_pcm(const int16_t* pcm, int64_t span, int ch, d
     return hipGetLastError();
 }
 
-// FindAttenuationDivider for every frame (one wave per frame)
+// FindAttenuationDivider for every frame (one 8-wave workgroup per frame)
 extern "C" hipError_t gsc_launch_atten(int cs, DspFrame* frames, int nframes, const double* samp, int64_t span, int ch,
                                        int obd, hipStream_t st) {
+    const size_t shm = size_t(2) * kAttBatch * 64 * sizeof(double);
     switch (cs) {
-    case 4: hipLaunchKernelGGL(atten_kernel<4>, dim3(nframes), dim3(64), 0, st, frames, nframes, samp, span, ch, obd); break;
-    case 8: hipLaunchKernelGGL(atten_kernel<8>, dim3(nframes), dim3(64), 0, st, frames, nframes, samp, span, ch, obd); break;
-    case 16: hipLaunchKernelGGL(atten_kernel<16>, dim3(nframes), dim3(64), 0, st, frames, nframes, samp, span, ch, obd); break;
+#define AK(CSV)                                                                                                  \
+    case CSV:                                                                                                    \
+        if (hipError_t e = hipFuncSetAttribute((const void*)atten_kernel<CSV>,                                   \
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm))            \
+            return e;                                                                                            \
+        hipLaunchKernelGGL(atten_kernel<CSV>, dim3(nframes), dim3(kAttThreads), shm, st, frames, nframes, samp,  \
+                           span, ch, obd);                                                                       \
+        break;
+        AK(4)
+        AK(8)
+        AK(16)
+#undef AK
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
