@@ -267,17 +267,20 @@ void Encoder::frame_host_src(FrameState& f) const {
     const int sc = f.sample_count;
     const int chunk_count = (sc - 1) / cs + 1;
     f.n = chunk_count * ch;
-    f.src.assign(size_t(f.n) * cs, 0.0);
     f.neg.assign(size_t(f.n), 0);
     f.rev.assign(size_t(f.n), 0);
-    for (int i = 0; i < chunk_count; ++i)
-        for (int j = 0; j < ch; ++j) {
-            double* s = &f.src[size_t(i * ch + j) * cs];
-            for (int k = 0; k < cs; ++k) {
-                const int pos = i * cs + k;
-                s[k] = pos >= sc ? 0.0 : 0.0 + filtered_[j][f.start + pos];
-            }
-        }
+}
+
+// chunk j's srcData (chunkRefs order: chunk-major, channel-minor; zero past
+// the frame's samples), read from the loaded samples (encoder.lpr:467-485)
+void Encoder::chunk_src(const FrameState& f, int j, double* out) const {
+    const int cs = opt_.chunk_size, ch = channels_;
+    const int i = j / ch, c = j - i * ch;
+    const double* row = filtered_[size_t(c)].data() + f.start;
+    for (int k = 0; k < cs; ++k) {
+        const int pos = i * cs + k;
+        out[k] = pos >= f.sample_count ? 0.0 : 0.0 + row[pos];
+    }
 }
 
 // TFrame.Reduce after the clustering (encoder.lpr:843-912)
@@ -300,9 +303,10 @@ void Encoder::frame_reduce_post(FrameState& f, bool reduced) const {
         const int K = opt_.chunks_per_frame, N = f.n;
         std::vector<double> acc(size_t(K) * cs, 0.0);
         std::vector<int> count(size_t(K), 0);
+        double s[16];
         for (int j = 0; j < N; ++j) {
             const int c = f.clusters[j];
-            const double* s = &f.src[size_t(j) * cs];
+            chunk_src(f, j, s);
             double* a = &acc[size_t(c) * cs];
             const double sg = f.neg[j] ? -1.0 : 1.0;
             for (int k = 0; k < cs; ++k) a[k] += s[f.rev[j] ? cs - 1 - k : k] * sg;
@@ -336,7 +340,11 @@ void Encoder::frame_reduce_post(FrameState& f, bool reduced) const {
         f.rdst.assign(size_t(N) * cs, 0);
         f.ratten.assign(size_t(N), 0);
         f.rneg.assign(size_t(N), 0);
-        for (int i = 0; i < N; ++i) make_reduced(i, &f.src[size_t(i) * cs]);
+        double s[16];
+        for (int i = 0; i < N; ++i) {
+            chunk_src(f, i, s);
+            make_reduced(i, s);
+        }
     }
 }
 

@@ -50,7 +50,6 @@ struct FrameState {
     int index = 0, start = 0, sample_count = 0;
     int atten_div = 6;
     int n = 0;                 // chunkRefs count (chunk-major, channel-minor)
-    std::vector<double> src;   // n*CS srcData
     std::vector<uint8_t> neg, rev;
     std::vector<int> red;      // final reduced-chunk index per chunk
     // reduced chunks
@@ -117,7 +116,8 @@ class Encoder {
     long long sample_count() const { return sample_count_; }
 
    private:
-    void frame_host_src(FrameState& f) const;  // chunk count + srcData (encoder.lpr:467-485)
+    void frame_host_src(FrameState& f) const;  // chunk count (encoder.lpr:467-485)
+    void chunk_src(const FrameState& f, int j, double* out) const;  // chunk j's srcData (CS doubles)
     // device DSP for frames (first frame index b): atten_div, neg / rev on the
     // host side, features left in the device slab *dX at (*xoff)[i]; with dQ,
     // also the KNNFit queries Single(srcData) (N*CS floats per frame, frames

@@ -1168,6 +1168,9 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
     const double t3 = now_ms();
     if (recon && device_recon(b, frames, recon, err) != 0) return -1;
     out->clear();
+    size_t bytes = 0;
+    for (auto& f : frames) bytes += f.stream.size();
+    out->reserve(bytes);
     for (auto& f : frames) out->insert(out->end(), f.stream.begin(), f.stream.end());
     double t4 = now_ms();
     if (std::getenv("GSC_HOST_TIMING"))
