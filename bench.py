@@ -12,7 +12,7 @@ contiguous frame range (balanced by chunk count) of an N-times longer signal
 (weak scaling) and rank 0 gathers the per-frame .gsc bytes (torch.distributed
 over RCCL/xGMI).
 
-python bench.py [--gpus N] [--steps K] [--warmup W] [--seconds S] [--config c2|c3|c1]
+python bench.py [--gpus N] [--steps K] [--warmup W] [--seconds S] [--config c2|c3|c1|c5|c5cs4]
 """
 from __future__ import annotations
 
@@ -31,6 +31,9 @@ CONFIGS = {
     "c2": (["-cs8", "-cpf4096", "-cbd8"], 2, 44100, 8, "44.1 kHz stereo, ChunkSize=8 ChunkCount=4096 8-bit"),
     "c3": (["-cs16", "-cpf4096", "-cbd12"], 2, 44100, 16, "44.1 kHz stereo, ChunkSize=16 ChunkCount=4096 12-bit"),
     "c1": (["-cs8", "-cpf256"], 1, 44100, 8, "mono, ChunkSize=8 ChunkCount=256 8-bit"),
+    # configs[4]'s signal (48 kHz stereo, ChunkCount=4096) at both ChunkSizes SURVEY.md §8 names
+    "c5": (["-cs8", "-cpf4096"], 2, 48000, 8, "48 kHz stereo, ChunkSize=8 ChunkCount=4096"),
+    "c5cs4": (["-cs4", "-cpf4096"], 2, 48000, 4, "48 kHz stereo, ChunkSize=4 ChunkCount=4096"),
 }
 
 VALU_F32_PEAK_TOPS = 78.6  # non-fused f32 VALU ops/s: half the 157.3 TFLOPS FMA-counted peak
@@ -194,8 +197,11 @@ def main():
                     None)
         if kern:
             traffic = kern["hbm_bytes_per_frame_per_launch"] * tm["reduce_frames"]
+    metric = "encoded Msamples/s @44.1kHz stereo ChunkSize=8 ChunkCount=4096; bit-exact .gsc"  # BASELINE.json
+    if args.config != "c2":
+        metric = f"encoded Msamples/s ({desc}); bit-exact .gsc"
     result = {
-        "metric": "encoded Msamples/s @44.1kHz stereo ChunkSize=8 ChunkCount=4096; bit-exact .gsc",
+        "metric": metric,
         "value": round(value, 4),
         "unit": "Msamples/s",
         "n_gpus": ws,
