@@ -78,7 +78,7 @@ typedef struct {
     double vfr;           /* -vfr, default 1.0 */
     int chunk_blend;      /* -cb, default 0 (only 0 supported) */
     double frame_length;  /* -fl, default 4000 ms */
-    int python_reduce;    /* -py (not supported by the GPU path) */
+    int python_reduce;    /* -py: cluster.py's Birch reducer instead of yakmo + KNNScanReduce */
     int verbose;          /* -v */
 } gsc_options;
 
@@ -147,6 +147,7 @@ typedef struct {
     double gpu_dsp_ms;           /* device DSP incl. sample upload (attenuation divider, features) */
     double post_overlap_ms;      /* KNNFit + prune/sort + packing run while other frames were still scanning */
     int post_groups;             /* frame groups the post-processing pipeline ran */
+    double gpu_recon_ms;         /* gsc_encode_wav_recon only: reconstruction + PsyADelta sum */
 } gsc_timing;
 void gsc_last_timing(gsc_timing *t);
 

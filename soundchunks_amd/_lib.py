@@ -56,6 +56,7 @@ class GscTiming(ctypes.Structure):
         ("gpu_dsp_ms", ctypes.c_double),
         ("post_overlap_ms", ctypes.c_double),
         ("post_groups", ctypes.c_int),
+        ("gpu_recon_ms", ctypes.c_double),
     ]
 
 

@@ -18,6 +18,8 @@
 
 #include <vector>
 
+#include "gsc_npblas.h"
+
 namespace gsc {
 namespace {
 
@@ -178,14 +180,12 @@ __global__ __launch_bounds__(kWardThreads) void ward_nn_chain_kernel(int n, doub
     }
 }
 
-__device__ __forceinline__ double dotf(const double* a, const double* b, int d) {  // np.dot (fma chain)
-    double s = 0.0;
-    for (int k = 0; k < d; ++k) s = fma(a[k], b[k], s);
-    return s;
-}
-
-// Birch._predict: argmin_c |x|^2 - 2 x.c + |c|^2 (sklearn ArgKmin, k = 1: the
-// first minimum); one thread per sample
+// Birch._predict = sklearn ArgKmin (k = 1) over EuclideanArgKmin64:
+// d = max(0, (|x|^2 + (-2 x.c)) + |c|^2) with |x|^2 from scipy's ddot
+// (_sqeuclidean_row_norms64), the middle term from scipy's dgemm (alpha = -2,
+// a sequential fma chain per element) and |c|^2 = Birch._subcluster_norms
+// (row_norms: einsum); heap_push keeps the first strict minimum.  One thread
+// per sample.
 __global__ __launch_bounds__(256) void birch_predict_kernel(int n, int d, const double* __restrict__ X, int m,
                                                             const double* __restrict__ C,
                                                             const double* __restrict__ cn,
@@ -193,13 +193,14 @@ __global__ __launch_bounds__(256) void birch_predict_kernel(int n, int d, const 
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const double* x = X + (int64_t)i * d;
-    const double xn = dotf(x, x, d);
+    const double xn = npblas::np_ddot(x, x, d);
     double best = INFINITY;
     int bi = 0;
     for (int j = 0; j < m; ++j) {
-        double v = -2.0 * dotf(x, C + (int64_t)j * d, d);
-        v = v + xn;
+        const double mid = -2.0 * npblas::seq_fma_dot(x, C + (int64_t)j * d, d);
+        double v = xn + mid;
         v = v + cn[j];
+        v = v > 0.0 ? v : 0.0;  // max(0., d): catastrophic cancellation
         if (v < best) {
             best = v;
             bi = j;
@@ -210,7 +211,7 @@ __global__ __launch_bounds__(256) void birch_predict_kernel(int n, int d, const 
 
 __global__ void row_norms_kernel(int m, int d, const double* __restrict__ C, double* __restrict__ cn) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < m) cn[j] = dotf(C + (int64_t)j * d, C + (int64_t)j * d, d);
+    if (j < m) cn[j] = npblas::np_einsum_sq(C + (int64_t)j * d, d);
 }
 
 template <typename T>
@@ -229,6 +230,11 @@ struct DBuf {
 extern "C" int gsc_ward_linkage_dev(int m, int d, const double* centers, double* Z) {
     if (m < 2) return 0;
     const int64_t nd = (int64_t)m * (m - 1) / 2;
+    {  // the condensed distance matrix must fit: refuse up front (-2) instead of failing mid-way
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return -1;
+        if ((size_t)nd * sizeof(double) + (size_t)m * (size_t)(d + 8) * sizeof(double) > free_b) return -2;
+    }
     DBuf<double> dX, dD, dZ;
     DBuf<int> dS, dC;
     if (!dX.alloc(size_t(m) * d) || !dD.alloc(size_t(nd)) || !dZ.alloc(size_t(m - 1) * 4) || !dS.alloc(size_t(m)) ||

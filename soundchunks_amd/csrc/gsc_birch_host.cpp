@@ -5,10 +5,15 @@
 // and returns Birch.labels_ (only the labels reach the encoder: cluster.py's
 // .cluster_centres are replaced by the cluster means of a5).  Restated here
 // natively, after the sklearn 1.7.2 / scipy 1.15 code the reference runs:
-//   1. the text round trip: every Single is printed with FloatToStr and read
-//      back by numpy.loadtxt as a double (modelled as 15 significant digits,
-//      FloatToStr's Extended precision on Win64; an assumption documented in
-//      DESIGN.md);
+//   1. the text round trip (extern.pas:363-369, cluster.py:13): every Single
+//      is printed by FloatToStr and read back by numpy.loadtxt as a double.
+//      FloatToStr(Single) in encoder.exe (@0x100034390 -> @0x100034340)
+//      widens to Double and calls FloatToStrFIntl(ffGeneral, Precision 15,
+//      Digits 0, fvSingle) (@0x100032a10), whose fvSingle branch
+//      (@0x100032b5c) is Str(Single(v):21) with real type single; str_real
+//      (@0x10000c240) caps the digits at its per-type table entry
+//      (.data 0x10004b950: single -> 10 digits, 2 exponent digits), so the
+//      text carries 10 significant digits: v -> strtod("%.9e" of v);
 //   2. the CF tree (sklearn/cluster/_birch.py: _CFNode.insert_cf_subcluster,
 //      _CFSubcluster.update / merge_subcluster, _split_node), in sample order;
 //   3. the global step AgglomerativeClustering(n_clusters = K) = Ward linkage
@@ -17,12 +22,14 @@
 //      stable sort by height, union-find relabelling) cut by sklearn's _hc_cut
 //      (a max-heap of node ids, labels in heap order);
 //   4. labels_ = the global label of each sample's nearest subcluster centroid
-//      (Birch._predict: argmin of |c|^2 - 2 x.c, first minimum).
-// Numerics: pdist is a sequential sum (bit-identical to scipy's, checked on
-// the committed fixtures); dot products are sequential fma chains (OpenBLAS's
-// ddot for n < 16); GEMM/gemv-based steps (node distances, predict) may
-// differ from numpy's BLAS in the last bit, which can only matter at exact
-// near-ties.  Labels equal cluster.py's on every committed fixture
+//      (Birch._predict -> sklearn ArgKmin: max(0, (|x|^2 + (-2 x.c)) + |c|^2),
+//      first minimum).
+// Numerics: every dot product, norm and product matrix follows the summation
+// order of the BLAS / einsum call numpy and scipy make for it (gsc_npblas.h:
+// np.dot of two vectors and scipy's _dot -> OpenBLAS ddot; np.dot(M, v) ->
+// dgemv_t; euclidean_distances in _split_node -> einsum row norms and dsyrk;
+// the predict middle term -> dgemm); pdist is a sequential sum (scipy's).
+// Labels equal cluster.py's on every committed fixture
 // (tests/golden/birch_*.npz, tools: tests/golden/make_birch.py).
 // The O(m^2) Ward step and the O(N m) predict run on the device
 // (gsc_birch.hip); the CF tree is sequential by construction and runs here.
@@ -34,6 +41,8 @@
 #include <string>
 #include <vector>
 
+#include "gsc_npblas.h"
+
 namespace gsc {
 
 extern "C" int gsc_ward_linkage_dev(int m, int d, const double* centers, double* Z);
@@ -44,11 +53,8 @@ namespace {
 constexpr double kThreshold = 0.001;
 constexpr int kBranching = 50;
 
-double dotf(const double* a, const double* b, int d) {  // np.dot of two vectors (fma chain)
-    double s = 0.0;
-    for (int k = 0; k < d; ++k) s = std::fma(a[k], b[k], s);
-    return s;
-}
+// np.dot of two vectors (OpenBLAS ddot order)
+double dotv(const double* a, const double* b, int d) { return npblas::np_ddot(a, b, d); }
 
 struct Sub {
     int n = 0;
@@ -101,7 +107,7 @@ class Birch {
         a.ss = a.ss + b.ss;
         a.centroid.resize(size_t(d_));
         for (int k = 0; k < d_; ++k) a.centroid[k] = a.ls[k] / double(a.n);
-        a.sqn = dotf(a.centroid.data(), a.centroid.data(), d_);
+        a.sqn = dotv(a.centroid.data(), a.centroid.data(), d_);
     }
 
     // _CFSubcluster.merge_subcluster
@@ -115,7 +121,7 @@ class Birch {
         const double inv = 1.0 / double(new_n);
         std::vector<double> c(static_cast<size_t>(d_));
         for (int k = 0; k < d_; ++k) c[k] = inv * new_ls[k];
-        const double new_sqn = dotf(c.data(), c.data(), d_);
+        const double new_sqn = dotv(c.data(), c.data(), d_);
         const double sq_radius = new_ss / double(new_n) - new_sqn;
         if (sq_radius <= kThreshold * kThreshold) {
             a.n = new_n;
@@ -147,15 +153,18 @@ class Birch {
         const std::vector<int> members = nodes_[node].subs;  // copy: the node is dropped
         const int m = int(members.size());
         const double* C = nodes_[node].cent.data();
-        const double* Y = nodes_[node].sqn.data();
+        // euclidean_distances(centroids_, squared=True) with Y = X: the passed
+        // Y_norm_squared is unused (Y is X); XX = row_norms (einsum), then
+        // -2 * (X @ X.T) (dsyrk) + XX[i] + XX[j], clipped at 0, zero diagonal
+        if (m != kBranching + 1) std::abort();  // _split_node only ever sees branching_factor + 1 rows
         std::vector<double> xx(static_cast<size_t>(m)), dist(size_t(m) * m);
-        for (int i = 0; i < m; ++i) xx[i] = dotf(C + size_t(i) * d_, C + size_t(i) * d_, d_);
+        for (int i = 0; i < m; ++i) xx[i] = npblas::np_einsum_sq(C + size_t(i) * d_, d_);
         for (int i = 0; i < m; ++i)
             for (int j = 0; j < m; ++j) {
-                double v = -2.0 * dotf(C + size_t(i) * d_, C + size_t(j) * d_, d_);
+                double v = -2.0 * npblas::np_syrk51(C, d_, i, j);
                 v = v + xx[i];
-                v = v + Y[j];
-                dist[size_t(i) * m + j] = i == j ? 0.0 : std::max(v, 0.0);
+                v = v + xx[j];
+                dist[size_t(i) * m + j] = i == j ? 0.0 : (v < 0.0 ? 0.0 : v);  // np.maximum(v, 0)
             }
         size_t far = 0;
         for (size_t k = 1; k < dist.size(); ++k)
@@ -187,7 +196,7 @@ class Birch {
         int best = 0;
         double bd = 0.0;
         for (int i = 0; i < m; ++i) {
-            double v = dotf(&nd.cent[size_t(i) * d_], q, d_);
+            double v = npblas::np_gemv_row(&nd.cent[size_t(i) * d_], q, d_, m, i);  // np.dot(centroids_, c)
             v = v * -2.0;
             v = v + nd.sqn[i];
             if (i == 0 || v < bd) {
@@ -234,7 +243,7 @@ class Birch {
             sb.n = 1;
             sb.ls.assign(X + size_t(i) * d_, X + size_t(i + 1) * d_);
             sb.centroid = sb.ls;
-            sb.ss = sb.sqn = dotf(sb.ls.data(), sb.ls.data(), d_);
+            sb.ss = sb.sqn = dotv(sb.ls.data(), sb.ls.data(), d_);
             if (insert(root, s)) {
                 const auto ns = split(root);
                 root = new_node(false);
@@ -362,11 +371,12 @@ std::vector<int> hc_cut(int K, const std::vector<int>& children, int n_leaves) {
 
 // labels of N samples (N x d Single) reduced to K clusters; 0 or an error
 int birch_reduce_labels(int n, int d, const float* feat, int K, int* labels, std::string* err) {
-    // FloatToStr -> numpy.loadtxt round trip (extern.pas:363-369, cluster.py:13)
+    // FloatToStr -> numpy.loadtxt round trip (extern.pas:363-369, cluster.py:13):
+    // 10 significant digits (FloatToStr(Single), see the header)
     std::vector<double> X(size_t(n) * d);
     char buf[64];
     for (size_t k = 0; k < X.size(); ++k) {
-        std::snprintf(buf, sizeof(buf), "%.15g", double(feat[k]));
+        std::snprintf(buf, sizeof(buf), "%.9e", double(feat[k]));
         X[k] = std::strtod(buf, nullptr);
     }
     Birch b(d);
@@ -378,7 +388,17 @@ int birch_reduce_labels(int n, int d, const float* feat, int K, int* labels, std
     } else {
         std::vector<double> Z(size_t(m > 1 ? m - 1 : 1) * 4);
         if (m > 1) {
-            if (gsc_ward_linkage_dev(m, d, centers.data(), Z.data()) != 0) {
+            const int wr = gsc_ward_linkage_dev(m, d, centers.data(), Z.data());
+            if (wr == -2) {
+                char msg[160];
+                std::snprintf(msg, sizeof(msg),
+                              "Birch: Ward linkage of %d subclusters needs %.1f GB of device memory for its "
+                              "condensed distance matrix, more than is free",
+                              m, double(m) * double(m - 1) / 2.0 * 8.0 / 1e9);
+                *err = msg;
+                return -1;
+            }
+            if (wr != 0) {
                 *err = "Birch: Ward linkage on the device failed";
                 return -1;
             }

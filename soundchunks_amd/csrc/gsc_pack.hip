@@ -60,13 +60,21 @@ __global__ __launch_bounds__(kPackThreads) void pack_kernel(PackFrame* __restric
                                                             uint32_t* __restrict__ codes_out) {
     __shared__ int wsum[kPackThreads / 64];
     __shared__ int carry;
+    __shared__ int overrun;
     PackFrame& f = frames[blockIdx.x];
     const int N = f.N;
     const int* b = best + f.out_off;
     const int* rm = remap + f.r_off;
     uint32_t* w = words + f.w_off;
+    // the slab's capacity: a code that would land past it is not written and
+    // the frame reports nbits = -1 (the 17-bit premise above broke), so a
+    // broken premise can never corrupt the next frame's slab
+    const int64_t cap = (int64_t(N) * 17 + 31) / 32 + 1;  // pack_word_capacity(N)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) carry = 0;
+    if (tid == 0) {
+        carry = 0;
+        overrun = 0;
+    }
     __syncthreads();
     for (int base = 0; base < N; base += kPackThreads * kPackPerThread) {
         const int j0 = base + tid * kPackPerThread;
@@ -123,15 +131,21 @@ __global__ __launch_bounds__(kPackThreads) void pack_kernel(PackFrame* __restric
         for (int e = 0; e < kPackPerThread; ++e) {
             if (size[e] == 0) continue;
             const int wi = bit >> 5, sh = bit & 31;
-            atomicOr(&w[wi], code[e] << sh);
-            if (sh + size[e] > 32) atomicOr(&w[wi + 1], code[e] >> (32 - sh));
+            const bool two = sh + size[e] > 32;
+            if (wi + (two ? 1 : 0) >= cap) {
+                overrun = 1;
+            } else {
+                atomicOr(&w[wi], code[e] << sh);
+                if (two) atomicOr(&w[wi + 1], code[e] >> (32 - sh));
+            }
             bit += size[e];
         }
         __syncthreads();  // everyone has read carry and wsum
         if (tid == 0) carry += total;
         __syncthreads();
     }
-    if (tid == 0) f.nbits = carry;
+    __syncthreads();
+    if (tid == 0) f.nbits = overrun ? -1 : carry;
 }
 
 }  // namespace gsc

@@ -146,6 +146,20 @@ struct DevBuf {
     }
 };
 
+// stream-ordered device buffer (hipMallocAsync / hipFreeAsync on one stream)
+template <typename T>
+struct StreamBuf {
+    T* p = nullptr;
+    hipStream_t st;
+    explicit StreamBuf(hipStream_t s) : st(s) {}
+    ~StreamBuf() {
+        if (p) (void)hipFreeAsync(p, st);
+    }
+    hipError_t alloc(size_t count) {
+        return hipMallocAsync(reinterpret_cast<void**>(&p), sizeof(T) * std::max<size_t>(count, 1), st);
+    }
+};
+
 // IntPower(10.0, -Precision) (encoder.lpr:761)
 double scan_tolerance(int precision) {
     if (precision <= 0) return 1.0;
@@ -357,7 +371,7 @@ int run_reduce_batch(int D, int K, int precision, const std::vector<int>& Ns, co
 // rule for every such query (gsc_ann.hip knnfit_ann_kernel).
 int run_knnfit_overflow(int CS, const std::vector<FitFrame>& fr, const std::vector<int>& ov_frames,
                         const std::vector<float>& eps, const std::vector<float>& cand, const std::vector<float>& q,
-                        std::vector<int>* best) {
+                        std::vector<int>* best, hipStream_t st) {
     const int nt = int(ov_frames.size());
     std::vector<float> pts;
     std::vector<int64_t> pt_off(static_cast<size_t>(nt)), nd_off(static_cast<size_t>(nt));
@@ -401,11 +415,13 @@ int run_knnfit_overflow(int CS, const std::vector<FitFrame>& fr, const std::vect
     }
     if (jobs.empty()) return 0;
     if (q.size() > size_t(INT32_MAX)) return fail("KNNFit overflow: query slab exceeds 2^31 floats");
-    DevBuf<float> dPts, dCv, dLo, dHi, dBnd, dQ, dPqk;
-    DevBuf<int> dPidx, dCd, dOut;
-    DevBuf<AnnTree> dTrees;
-    DevBuf<KnnOvJob> dJobs;
-    DevBuf<int4> dPqn;
+    // stream-ordered buffers: the replay runs on the caller's stream (the
+    // post-processing stream during the scan) and never syncs the device
+    StreamBuf<float> dPts(st), dCv(st), dLo(st), dHi(st), dBnd(st), dQ(st), dPqk(st);
+    StreamBuf<int> dPidx(st), dCd(st), dOut(st);
+    StreamBuf<AnnTree> dTrees(st);
+    StreamBuf<KnnOvJob> dJobs(st);
+    StreamBuf<int4> dPqn(st);
     HIP_TRY(dPts.alloc(pts.size()));
     HIP_TRY(dPidx.alloc(size_t(pts.size() / size_t(CS))));
     HIP_TRY(dCd.alloc(size_t(nodes)));
@@ -416,10 +432,10 @@ int run_knnfit_overflow(int CS, const std::vector<FitFrame>& fr, const std::vect
     HIP_TRY(dTrees.alloc(size_t(nt)));
     HIP_TRY(dQ.alloc(q.size()));
     HIP_TRY(dOut.alloc(best->size()));
-    HIP_TRY(hipMemcpy(dPts.p, pts.data(), sizeof(float) * pts.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemset(dCd.p, 0xff, sizeof(int) * size_t(nodes)));
-    HIP_TRY(hipMemcpy(dQ.p, q.data(), sizeof(float) * q.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(dOut.p, best->data(), sizeof(int) * best->size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpyAsync(dPts.p, pts.data(), sizeof(float) * pts.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(dCd.p, 0xff, sizeof(int) * size_t(nodes), st));
+    HIP_TRY(hipMemcpyAsync(dQ.p, q.data(), sizeof(float) * q.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(dOut.p, best->data(), sizeof(int) * best->size(), hipMemcpyHostToDevice, st));
     std::vector<AnnTree> trees(static_cast<size_t>(nt));
     for (int t = 0; t < nt; ++t) {
         AnnTree& a = trees[size_t(t)];
@@ -433,8 +449,8 @@ int run_knnfit_overflow(int CS, const std::vector<FitFrame>& fr, const std::vect
         a.hi = dHi.p + nd_off[t];
         a.bnd = dBnd.p + size_t(2 * CS) * size_t(t);
     }
-    HIP_TRY(hipMemcpy(dTrees.p, trees.data(), sizeof(AnnTree) * size_t(nt), hipMemcpyHostToDevice));
-    HIP_TRY(gsc_launch_ann_build_many(dTrees.p, nt, nullptr));
+    HIP_TRY(hipMemcpyAsync(dTrees.p, trees.data(), sizeof(AnnTree) * size_t(nt), hipMemcpyHostToDevice, st));
+    HIP_TRY(gsc_launch_ann_build_many(dTrees.p, nt, st));
     // the box queues (<= one push per split node each): bounded launches
     const int pq_cap = max_n + 2;
     const size_t per_job = size_t(pq_cap) * (sizeof(float) + sizeof(int4));
@@ -442,13 +458,13 @@ int run_knnfit_overflow(int CS, const std::vector<FitFrame>& fr, const std::vect
     HIP_TRY(dPqk.alloc(size_t(chunk) * pq_cap));
     HIP_TRY(dPqn.alloc(size_t(chunk) * pq_cap));
     HIP_TRY(dJobs.alloc(jobs.size()));
-    HIP_TRY(hipMemcpy(dJobs.p, jobs.data(), sizeof(KnnOvJob) * jobs.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpyAsync(dJobs.p, jobs.data(), sizeof(KnnOvJob) * jobs.size(), hipMemcpyHostToDevice, st));
     for (size_t j0 = 0; j0 < jobs.size(); j0 += size_t(chunk)) {
         const int nj = int(std::min<size_t>(size_t(chunk), jobs.size() - j0));
-        HIP_TRY(gsc_launch_knnfit_ann(dTrees.p, dJobs.p + j0, nj, dQ.p, dOut.p, dPqk.p, dPqn.p, pq_cap, nullptr));
+        HIP_TRY(gsc_launch_knnfit_ann(dTrees.p, dJobs.p + j0, nj, dQ.p, dOut.p, dPqk.p, dPqn.p, pq_cap, st));
     }
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(best->data(), dOut.p, sizeof(int) * best->size(), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpyAsync(best->data(), dOut.p, sizeof(int) * best->size(), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
     for (const KnnOvJob& j : jobs)
         if ((*best)[size_t(j.out)] < 0) return fail("KNNFit: ANN priority search emulation failed");
     return 0;
@@ -514,7 +530,7 @@ int run_knnfit_batch(int CS, const std::vector<int>& Rs, const std::vector<int>&
             qh.resize(size_t(qo));
             HIP_TRY(hipMemcpy(qh.data(), qdev, sizeof(float) * size_t(qo), hipMemcpyDeviceToHost));
         }
-        if (run_knnfit_overflow(CS, fr, ov_frames, eps, cand, q.empty() ? qh : q, best) != 0) return -1;
+        if (run_knnfit_overflow(CS, fr, ov_frames, eps, cand, q.empty() ? qh : q, best, nullptr) != 0) return -1;
         if (knn_ms) *knn_ms += now_ms() - t0;
     }
     return 0;
@@ -854,7 +870,7 @@ int Encoder::post_group(std::vector<FrameState>& frames, const std::vector<int>&
             lf.push_back(x);
         }
         if (!chk(hipStreamSynchronize(st), "download")) return -1;
-        if (run_knnfit_overflow(cs, lf, lidx, leps, lcand, lq, &lbest) != 0) {
+        if (run_knnfit_overflow(cs, lf, lidx, leps, lcand, lq, &lbest, st) != 0) {
             *err = t_err;
             return -1;
         }
@@ -894,7 +910,7 @@ int Encoder::post_group(std::vector<FrameState>& frames, const std::vector<int>&
     for (int k = 0; ok && k < g; ++k) {
         const size_t i = size_t(ids[k]);
         const int64_t nw = (int64_t(pk[size_t(k)].nbits) + 31) / 32;  // whole u32 words (>= the 16-bit words used)
-        if (nw > pack_word_capacity(frames[i].n)) {
+        if (pk[size_t(k)].nbits < 0 || nw > pack_word_capacity(frames[i].n)) {  // pack_kernel refused the overrun
             *err = "index packer overran its word slab";
             return -1;
         }
@@ -997,6 +1013,14 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
     long long passes = 0, slow = 0, restarts = 0;
     // --- the KNNFit / prune / packing pipeline's slabs (whole range, allocated
     // before the scan starts: nothing is allocated or freed while it runs)
+    // the shared pinned arena is held for the whole encode, and released only
+    // after pc's stream and every device launch of this encode have drained
+    // (members are destroyed in reverse order: drain, pc, then the lock)
+    PinnedArena& pa = pinned_arena();
+    std::lock_guard<std::mutex> arena_lock(pa.m);
+    struct DeviceDrain {
+        ~DeviceDrain() { (void)hipDeviceSynchronize(); }
+    } drain_before_unlock;
     PostCtx pc;
     pc.recon = recon != nullptr;
     pc.dQry = dQry.p;
@@ -1016,8 +1040,6 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
         nw += pack_word_capacity(frames[i].n);
         nn += frames[i].n;
     }
-    PinnedArena& pa = pinned_arena();
-    std::lock_guard<std::mutex> arena_lock(pa.m);
     int64_t nred_pts = 0;
     for (int n : Ns) nred_pts += n;
     {
@@ -1167,6 +1189,7 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
     const double t2 = t_scan_end;
     const double t3 = now_ms();
     if (recon && device_recon(b, frames, recon, err) != 0) return -1;
+    const double recon_ms = now_ms() - t3;
     out->clear();
     size_t bytes = 0;
     for (auto& f : frames) bytes += f.stream.size();
@@ -1192,7 +1215,8 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
         tim->gpu_yakmo_ms = yak_ms;
         tim->gpu_scan_ms = scan_ms;
         tim->gpu_knnfit_ms = pc.knn_ms;
-        tim->host_post_ms = t4 - t2;  // what the post-processing adds after the scan
+        tim->host_post_ms = t4 - t2 - recon_ms;  // what the post-processing adds after the scan
+        tim->gpu_recon_ms = recon_ms;
         tim->post_overlap_ms = overlap_ms;
         tim->post_groups = pc.groups;
         tim->frames = nfr;
@@ -1396,10 +1420,12 @@ int gsc_encode_wav_recon(const uint8_t* wav, size_t wav_len, const gsc_options* 
         return fail("gsc_encode_wav_recon: null argument");
     *out = nullptr;
     *recon = nullptr;
+    t_tim = gsc_timing{};
     const double t0 = now_ms();
     Encoder enc(*o);
     std::string err;
     if (enc.prepare(wav, wav_len, &err) != 0) return fail(err);
+    t_tim.host_prepare_ms = now_ms() - t0;
     const int ch = enc.channels();
     const size_t n = size_t(enc.sample_count()) * size_t(ch);
     ReconOut ro;

@@ -48,6 +48,18 @@ def _quiet_tone(seconds=3.0, frac=0.6, rate=44100, seed=5):
     return wav_header(1, rate, n) + x.astype("<i2").tobytes()
 
 
+def _tone_lsb(seconds=4.5, rate=44100, seed=7):
+    """Mono 220 Hz tone with +-1 LSB noise: full 4-s frames (N ~ 44100 chunks at
+    ChunkSize 4) whose Birch subclusters stay in the thousands (the -py case)."""
+    from soundchunks_amd.synth import wav_header
+
+    rng = np.random.default_rng(seed)
+    n = int(seconds * rate)
+    t = np.arange(n) / rate
+    x = np.round(0.3 * np.sin(2 * np.pi * 220 * t) * 32767).astype(np.int64) + rng.integers(-1, 2, size=n)
+    return wav_header(1, rate, n) + x.astype("<i2").tobytes()
+
+
 def _tiny():
     """0.02 s: fewer chunks than ChunksPerFrame -> passthrough mode (encoder.lpr:891-912)."""
     return _synth(0.02)

@@ -4,7 +4,8 @@
 
 For each case, the frame's Reduce dataset (a1 staging, from the oracle trace)
 is written the way DoExternalSKLearn does (extern.pas:363-369: "i v0 v1 ... "
-per row; FloatToStr modelled as 15 significant digits), cluster.py is run on
+per row; FloatToStr(Single) prints 10 significant digits -- encoder.exe's
+str_real digit table, see soundchunks_amd/csrc/gsc_birch_host.cpp), cluster.py is run on
 it exactly as extern.pas:389-393 invokes it (-i FILE -n K -t 10^(1-Precision)),
 and the .membership labels are stored with the dataset (float32) in
 tests/golden/birch_<case>.npz.  The GPU test feeds the same dataset to the
@@ -37,8 +38,13 @@ BIRCH_CASES = {
 }
 
 
+def fpc_single_text(v: float) -> str:
+    """FloatToStr(Single): 10 significant digits (the value numpy.loadtxt reads back)."""
+    return "%.9E" % float(v)
+
+
 def dataset_text(x: np.ndarray) -> str:
-    return "".join(str(i) + " " + "".join("%.15g " % float(v) for v in row) + "\n" for i, row in enumerate(x))
+    return "".join(str(i) + " " + "".join(fpc_single_text(v) + " " for v in row) + "\n" for i, row in enumerate(x))
 
 
 def main(names):
@@ -66,7 +72,19 @@ if __name__ == "__main__" and sys.argv[1:2] != ["--files"]:
 # whole-file -py golden: the reference's own -py invocation on a corpus file
 # ("-fl500 -cpf256 -py"); cluster.py labels for every reduced
 # frame, then the oracle encodes with them (oracle_ffi.set_py_labels)
-PY_FILES = {"mstest_fl500_cpf256_py": ("lame_test/mstest.wav", ["-fl500", "-cpf256", "-py"])}
+PY_FILES = {
+    "mstest_fl500_cpf256_py": ("lame_test/mstest.wav", ["-fl500", "-cpf256", "-py"]),
+    # full-length frames: 4.5 s mono at ChunkSize 4 -> N ~ 44100 chunks per frame
+    "tone_lsb45_cs4_cpf256_py": ("tone_lsb45", ["-cs4", "-cpf256", "-py"]),
+}
+
+
+def py_file_wav(rel: str) -> bytes:
+    if rel == "tone_lsb45":
+        from golden.cases import _tone_lsb
+
+        return _tone_lsb(seconds=4.5)
+    return (HERE / rel).read_bytes()
 
 
 def make_py_file(name):
@@ -74,7 +92,7 @@ def make_py_file(name):
     import json
 
     rel, argv = PY_FILES[name]
-    wav = (HERE / rel).read_bytes()
+    wav = py_file_wav(rel)
     base = [a for a in argv if a != "-py"]
     _, nfr = oracle_ffi.encode_frames(wav, base, 0, 1)
     labels, offsets = [], []
@@ -110,5 +128,5 @@ def make_py_file(name):
 
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "--files":
-    for n in PY_FILES:
+    for n in sys.argv[2:] or PY_FILES:
         make_py_file(n)

@@ -193,37 +193,36 @@ def test_reconstruction_matches_oracle(oracle, name):
 
 
 # a9: the -py reducer (cluster.py Birch, sklearn 1.7.2) on the datasets the
-# reference hands it; labels from the real cluster.py (tests/golden/make_birch.py)
-_BIRCH_EXACT = ["mstest_fl500_f0", "mstest_fl500_f2", "silence_tone_cs8_cpf256_f0", "c1_test_cs8_cpf256_f1"]
+# reference hands it; labels from the real cluster.py (tests/golden/make_birch.py),
+# bit for bit (the numpy / scipy BLAS summation orders: gsc_npblas.h)
+_BIRCH = ["mstest_fl500_f0", "mstest_fl500_f2", "silence_tone_cs8_cpf256_f0", "c1_test_cs8_cpf256_f1",
+          "hihat_cs8_cpf256_f0"]
 
 
-@pytest.mark.parametrize("name", _BIRCH_EXACT + ["hihat_cs8_cpf256_f0"])
+@pytest.mark.parametrize("name", _BIRCH)
 def test_birch_labels_match_cluster_py(name):
     from golden.cases import HERE
     from soundchunks_amd.encoder import birch_labels
 
     z = np.load(HERE / f"birch_{name}.npz")
     got = birch_labels(z["dataset"], int(z["k"]))
-    bad = int((got != z["labels"]).sum())
-    if name in _BIRCH_EXACT:
-        assert bad == 0
-    else:
-        # the predict step's dot products follow numpy/OpenBLAS summation
-        # order, which is not pinned: a handful of near-tied samples may flip
-        # (7 of 13951 on this dataset with the CPU restatement)
-        assert bad <= len(got) // 1000, bad
+    assert int((got != z["labels"]).sum()) == 0
 
 
-def test_python_reduce_file_matches_golden():
+@pytest.mark.parametrize("name", ["mstest_fl500_cpf256_py", "tone_lsb45_cs4_cpf256_py"])
+def test_python_reduce_file_matches_golden(name):
     import hashlib
     import json
 
     import soundchunks_amd as sc
     from golden.cases import HERE
+    from golden.make_birch import PY_FILES, py_file_wav
 
-    want = json.loads((HERE / "golden_meta.json").read_text())["mstest_fl500_cpf256_py"]
-    wav = (HERE / "lame_test" / "mstest.wav").read_bytes()
+    want = json.loads((HERE / "golden_meta.json").read_text())[name]
+    wav = py_file_wav(PY_FILES[name][0])
     assert hashlib.sha256(wav).hexdigest() == want["wav_sha256"]
     got = sc.Encoder(want["argv"]).encode(wav)
-    assert got == (HERE / "mstest_fl500_cpf256_py.gsc").read_bytes()
+    assert got == (HERE / f"{name}.gsc").read_bytes()
     assert hashlib.sha256(got).hexdigest() == want["gsc_sha256"]
+
+

@@ -2,9 +2,12 @@
 // host restatements of the two device steps, to compare labels with the
 // cluster.py fixtures on a machine without a GPU.
 //   g++ -O2 -ffp-contract=off -shared -fPIC -o /tmp/birch_host.so tools/birch/host_check.cpp soundchunks_amd/csrc/gsc_birch_host.cpp
+// (tests/test_birch_host.py builds and runs it against the cluster.py fixtures)
 #include <cmath>
 #include <string>
 #include <vector>
+
+#include "../../soundchunks_amd/csrc/gsc_npblas.h"
 
 namespace gsc {
 int birch_reduce_labels(int n, int d, const float* feat, int K, int* labels, std::string* err);
@@ -77,23 +80,19 @@ extern "C" int gsc_ward_linkage_dev(int n, int d, const double* X, double* Z) {
     }
     return 0;
 }
-static double dotf(const double* a, const double* b, int d) {
-    double s = 0.0;
-    for (int k = 0; k < d; ++k) s = std::fma(a[k], b[k], s);
-    return s;
-}
+// Birch._predict on the host (gsc_birch.hip birch_predict_kernel restated)
 extern "C" int gsc_birch_predict_dev(int n, int d, const double* X, int m, const double* C, int* out) {
     std::vector<double> cn(static_cast<size_t>(m));
-    for (int j = 0; j < m; ++j) cn[j] = dotf(C + size_t(j) * d, C + size_t(j) * d, d);
+    for (int j = 0; j < m; ++j) cn[j] = npblas::np_einsum_sq(C + size_t(j) * d, d);
     for (int i = 0; i < n; ++i) {
         const double* x = X + size_t(i) * d;
-        const double xn = dotf(x, x, d);
+        const double xn = npblas::np_ddot(x, x, d);
         double best = INFINITY;
         int bi = 0;
         for (int j = 0; j < m; ++j) {
-            double v = -2.0 * dotf(x, C + size_t(j) * d, d);
-            v = v + xn;
+            double v = xn + -2.0 * npblas::seq_fma_dot(x, C + size_t(j) * d, d);
             v = v + cn[j];
+            v = v > 0.0 ? v : 0.0;
             if (v < best) {
                 best = v;
                 bi = j;
