@@ -1,18 +1,30 @@
 """bench.py -- SoundChunks encode throughput on MI355X (driver contract).
 
 Metric (BASELINE.json): encoded Msamples/s @44.1 kHz stereo, ChunkSize=8,
-ChunkCount=4096 (configs[1]), bit-exact .gsc.  The job's one-off host pass
-(Load + PrepareFrames: the sequential frame-boundary scan of the whole file,
-encoder.lpr:1294-1429) runs once before timing and is reported as prepare_ms.
-One step = one encode of this rank's frames of a synthetic 44.1 kHz stereo
-signal (0.25 sin(440/660 Hz) + 0.05 N(0,1), PCG64(20250217)):
-per-frame sample staging and DSP, GPU Reduce (yakmo + KNNScanReduce) and
-KNNFit, bit packing.  Frames are independent: with N GPUs each rank encodes a
-contiguous frame range (balanced by chunk count) of an N-times longer signal
-(weak scaling) and rank 0 gathers the per-frame .gsc bytes (torch.distributed
-over RCCL/xGMI).
+ChunkCount=4096 (configs[1]), bit-exact .gsc, measured from the in-memory WAV
+to the .gsc bytes.
 
-python bench.py [--gpus N] [--steps K] [--warmup W] [--seconds S] [--config c2|c3|c1|c5|c5cs4]
+One step = one whole encode job of a synthetic WAV (SURVEY.md §8d signal:
+0.25 sin(440/660 Hz) + 0.05 N(0,1), PCG64(20250217)):
+  Load + PrepareFrames of the whole file (rank 0: the sequential frame-cut
+  scan, encoder.lpr:1294-1429, run by gsc_prepare), the frame boundaries
+  broadcast to every rank, then each rank's frame range (contiguous, balanced
+  by chunk count -- SURVEY.md §8e LPT): sample staging, device DSP, yakmo +
+  KNNScanReduce, KNNFit, bit packing; rank 0 gathers the frame-ordered .gsc
+  bytes (torch.distributed over RCCL/xGMI).
+The job's PrepareFrames is a host pass; rank 0 runs the next job's while the
+GPUs encode the current one (a streaming encoder's double buffering), so the
+timed region holds every job's prepare and every job's encode, and only the
+first job's prepare is exposed.  `job_latency_ms` is one job run alone.
+
+Scaling: weak by default (each rank adds --seconds of audio to one longer
+file); --strong keeps one --seconds file for any world size.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--seconds S]
+                  [--config c1|c2|c3|c4|c5|c5cs4] [--strong] [--no-cpu-baseline]
+
+--gpus N without a launcher's WORLD_SIZE spawns N worker processes (one per
+GPU, RANK/LOCAL_RANK/WORLD_SIZE, rendezvous at 127.0.0.1) before any GPU call.
 """
 from __future__ import annotations
 
@@ -21,6 +33,7 @@ import json
 import os
 import sys
 import time
+from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
@@ -34,7 +47,10 @@ CONFIGS = {
     # configs[4]'s signal (48 kHz stereo, ChunkCount=4096) at both ChunkSizes SURVEY.md §8 names
     "c5": (["-cs8", "-cpf4096"], 2, 48000, 8, "48 kHz stereo, ChunkSize=8 ChunkCount=4096"),
     "c5cs4": (["-cs4", "-cpf4096"], 2, 48000, 4, "48 kHz stereo, ChunkSize=4 ChunkCount=4096"),
+    # configs[3]: the reference's lame_test corpus (22 mono 44.1 kHz files) as one batch, default flags
+    "c4": (["-cs8", "-cpf4096"], 1, 44100, 8, "lame_test corpus (22 mono 44.1 kHz files), ChunkSize=8 ChunkCount=4096"),
 }
+CORPUS = ROOT / "tests" / "golden" / "lame_test"
 
 VALU_F32_PEAK_TOPS = 78.6  # non-fused f32 VALU ops/s: half the 157.3 TFLOPS FMA-counted peak
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md (spec)
@@ -56,14 +72,15 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(argv, rate: int, channels: int, frame_seconds: float, threads: int, runs: int = 3) -> dict:
+def cpu_baseline(cfg: str, argv, rate: int, channels: int, frame_seconds: float, threads: int,
+                 runs: int = 3) -> dict:
     """SURVEY.md §8d CPU baseline: the oracle (C restatement of the reference
     encoder, oracle/), frame-parallel like the reference's MTProcs pool
     (encoder.lpr:1449).  Single thread: `runs` independent 1-thread encodes of
-    one full frame, run side by side on separate cores (ctypes releases the
-    GIL), median.  All-core: `threads` threads on `threads` full frames of the
-    same signal and flags, one run (a full frame takes ~1.5 min on one core, so
-    three all-core runs would triple the bench's wall time)."""
+    one full frame side by side on separate cores (ctypes releases the GIL),
+    median.  All-core: `threads` threads on `threads` full frames of the same
+    signal and flags (c4: the corpus files in order until `threads` frames),
+    one run."""
     import statistics
     import threading
 
@@ -72,8 +89,21 @@ def cpu_baseline(argv, rate: int, channels: int, frame_seconds: float, threads: 
     from soundchunks_amd.synth import synth_wav
 
     oracle_ffi.load()
-    one_wav = synth_wav(frame_seconds, rate, channels)
-    one_samples = int(round(frame_seconds * rate)) * channels
+    if cfg == "c4":
+        wavs = [(CORPUS / n).read_bytes() for n in sorted(os.listdir(CORPUS)) if n.endswith(".wav")]
+        nfr = [len(oracle_ffi.frame_bounds(w, argv)[0]) for w in wavs]
+        one_wav = wavs[int(max(range(len(wavs)), key=lambda i: len(wavs[i]) / max(1, nfr[i])))]
+        one_wav = oracle_ffi_first_frame_wav(one_wav, argv)
+        sample, acc = [], 0
+        for w, f in zip(wavs, nfr):
+            if acc >= threads:
+                break
+            sample.append(w)
+            acc += f
+    else:
+        one_wav = synth_wav(frame_seconds, rate, channels)
+        sample = [synth_wav(frame_seconds * threads, rate, channels)]
+    one_samples = (len(one_wav) - 44) // 2
     walls = [0.0] * runs
 
     def run(i):
@@ -87,97 +117,170 @@ def cpu_baseline(argv, rate: int, channels: int, frame_seconds: float, threads: 
     for t in ths:
         t.join()
     w1 = statistics.median(walls)
-    many = frame_seconds * threads
-    wav = synth_wav(many, rate, channels)
     t = time.perf_counter()
-    oracle_ffi.encode(wav, argv, threads=threads)
+    if len(sample) == 1:
+        oracle_ffi.encode(sample[0], argv, threads=threads)
+    else:  # corpus files side by side, one encode per thread slot
+        from concurrent.futures import ThreadPoolExecutor as TP
+
+        with TP(threads) as pool:
+            list(pool.map(lambda w: oracle_ffi.encode(w, argv, threads=1), sample))
     wn = time.perf_counter() - t
-    allv = int(round(many * rate)) * channels / wn / 1e6
+    nsamp = sum((len(w) - 44) // 2 for w in sample)
+    allv = nsamp / wn / 1e6
     try:
         share = len(os.sched_getaffinity(0))
     except AttributeError:
         share = os.cpu_count()
+    what = (f"{len(sample)} corpus files ({nsamp / rate:.1f} s)" if cfg == "c4"
+            else f"{threads} full {frame_seconds:g}-s frames ({frame_seconds * threads:g} s) of the same synthetic "
+                 f"{rate} Hz {channels}-ch signal and flags")
     return {"value": round(allv, 6), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"all-core: {threads} full {frame_seconds:g}-s frames ({many:g} s) of the same synthetic "
-                      f"{rate} Hz {channels}-ch signal and flags, oracle/ C restatement frame-parallel on {threads} "
-                      f"threads, 1 run ({wn:.1f} s); single-thread: one full frame, median of {runs} side-by-side runs",
+            "sample": f"all-core: {what}, oracle/ C restatement frame-parallel on {threads} threads, 1 run "
+                      f"({wn:.1f} s); single-thread: one full frame, median of {runs} side-by-side runs",
             "single_thread": {"value": round(one_samples / w1 / 1e6, 6), "cores": 1, "wall_s": round(w1, 2),
-                              "runs_s": [round(w, 2) for w in walls], "seconds_of_audio": frame_seconds},
-            "all_core": {"value": round(allv, 6), "cores": threads, "wall_s": round(wn, 2), "seconds_of_audio": many},
+                              "runs_s": [round(w, 2) for w in walls]},
+            "all_core": {"value": round(allv, 6), "cores": threads, "wall_s": round(wn, 2)},
             "cpu_model": _cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": share}
+
+
+def oracle_ffi_first_frame_wav(wav: bytes, argv) -> bytes:
+    """The first frame of a corpus file as its own WAV (the single-thread leg)."""
+    import oracle_ffi
+    import struct
+
+    st, en = oracle_ffi.frame_bounds(wav, argv)
+    ch = struct.unpack_from("<H", wav, 22)[0]
+    n = int(en[0]) + 1
+    body = wav[44: 44 + n * ch * 2]
+    return wav[:40] + struct.pack("<I", len(body)) + body
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--seconds", type=float, default=1024.0,
-                    help="audio seconds per GPU (1024 s = 256 frames of 4 s: one frame per CU)")
+                    help="audio seconds per GPU (weak) or in total (--strong); 1024 s = 256 frames of 4 s")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--strong", action="store_true", help="one fixed-length file for any world size")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="all-core CPU baseline threads (the GPU box's CPU share is 16 per GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
     ws, rank, local = _dist_env()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        from soundchunks_amd.shard import spawn_workers
+
+        sys.exit(spawn_workers(args.gpus, [sys.executable, str(Path(__file__).resolve())] + sys.argv[1:]))
+    if ws != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
+        sys.exit(2)
+
+    import numpy as np
     import torch
 
     dist = None
+    dev = torch.device("cuda", local)
     if ws > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
     import soundchunks_amd as sc
-    from soundchunks_amd.shard import frame_range_weighted, gather_streams
+    from soundchunks_amd.shard import bounds_range, broadcast_bounds, gather_streams
     from soundchunks_amd.synth import synth_wav
 
     if ws > 1:
         sc.set_device(local)
 
     argv, ch, rate, cs, desc = CONFIGS[args.config]
-    total_seconds = args.seconds * ws
-    wav = synth_wav(total_seconds, rate, ch)
     enc = sc.Encoder(argv)
-    # Load + PrepareFrames once per job (the sequential frame-boundary scan of
-    # the whole file, encoder.lpr:1294-1429); each step encodes this rank's
-    # frame range, balanced by chunk count (SURVEY.md §8e LPT)
-    prep = enc.prepare(wav)
-    nframes = prep.frame_count
-    b, e = frame_range_weighted(prep.frame_chunks().tolist(), rank, ws)
+    if args.config == "c4":
+        return bench_corpus(args, enc, argv, desc, ws, rank, local, dist)
+    total_seconds = args.seconds if args.strong else args.seconds * ws
+    wav = synth_wav(total_seconds, rate, ch)  # the job's input, in host memory on every rank
 
-    def step():
-        out = prep.encode(b, e)
-        if dist is not None:  # frame-ordered .gsc on rank 0: one padded all-gather (RCCL over xGMI)
-            out = gather_streams(out, device=torch.device("cuda", local))
-        return out
+    pool = ThreadPoolExecutor(1) if rank == 0 else None
 
-    for _ in range(args.warmup):
-        step()
+    def prepare_job():  # rank 0: Load + PrepareFrames of the whole file (encoder.lpr:1111-1152, 1294-1429)
+        t = time.perf_counter()
+        p = enc.prepare(wav)
+        st, en = p.frame_bounds()
+        return p, st, en, (time.perf_counter() - t) * 1e3
+
+    info = {}
+
+    def step(fut, prefetch: bool):
+        """One job: consume this job's prepare (rank 0), start the next one's,
+        broadcast the frame bounds, encode this rank's frames, gather."""
+        p = st = en = None
+        nxt = None
+        if rank == 0:
+            p, st, en, info["prepare_ms"] = fut.result()
+            if prefetch:
+                nxt = pool.submit(prepare_job)
+        if dist is not None:  # rank 0's PrepareFrames boundaries to every rank
+            st, en = broadcast_bounds(st, en, device=dev)
+        b, e = bounds_range(st, en, cs, ch, rank, ws)
+        info["frames"], info["range"] = len(st), (b, e)
+        if rank == 0:
+            out = p.encode(b, e)
+        else:
+            out = enc.prepare_frames(wav, st, en, b, e).encode(b, e)
+        if dist is not None:
+            out = gather_streams(out, device=dev)
+        return out, nxt
+
+    # warmup (untimed): the first one, run alone, is the single-job latency
+    lat = None
+    for w in range(args.warmup):
+        t = time.perf_counter()
+        step(pool.submit(prepare_job) if rank == 0 else None, False)
+        torch.cuda.synchronize()
+        if w == 0:
+            lat = (time.perf_counter() - t) * 1e3
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    fut = pool.submit(prepare_job) if rank == 0 else None
     timings = []
-    for _ in range(args.steps):
-        step()
+    for k in range(args.steps):
+        _, fut = step(fut, k + 1 < args.steps)
         timings.append(sc.Encoder.last_timing())
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([dt], device="cuda")
+        t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     if rank != 0:
         dist.destroy_process_group()
         return
-
     n_samples = int(round(total_seconds * rate)) * ch
     value = n_samples * args.steps / dt / 1e6
-    tm = timings[-1]
+    result = base_result(args, ws, dt, value, desc, enc, timings[-1], cs, argv, rate, ch)
+    result["config"] = {"workload": f"{desc}, {total_seconds:g} s synthetic", "frames": info["frames"],
+                        "argv": argv, "parallelism": f"frame-sharded x{ws}", "rank0_frames": list(info["range"])}
+    result["data"] = (f"synthetic (SURVEY.md §8d tone+noise, PCG64 20250217), "
+                      f"{total_seconds:g} s {'in total' if args.strong else f'= {args.seconds:g} s per GPU'}")
+    result["prepare_ms"] = round(info["prepare_ms"], 1)
+    result["job_latency_ms"] = None if lat is None else round(lat, 1)
+    result["realtime_x"] = round(value / (rate * ch / 1e6), 2)
+    if not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args.config, argv, rate, ch, enc.frame_length / 1000.0,
+                                              args.cpu_threads)
+    print(json.dumps(result))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def base_result(args, ws, dt, value, desc, enc, tm, cs, argv, rate, ch) -> dict:
     # dominant kernel: KNNScanReduce passes; algorithmic ops = searches x K x 2CS x 3
     # (sub + mul + add per feature, SURVEY.md §8d: 6K ops per input sample per pass)
     K = enc.options.chunks_per_frame
@@ -191,16 +294,15 @@ def main():
     traffic = None
     if PMC_SUMMARY.exists():
         ks = json.loads(PMC_SUMMARY.read_text())["kernels"]
-        # the scan kernel's instance at this D and K = 4096 (ScanCfg<D, 12, slots, CUs>)
         kern = next((v for k, v in ks.items()
                      if k.startswith("gsc::scan_batch_kernel") and (f"<{2 * cs}, 12," in k or f"<{2 * cs}, 12>" in k)),
                     None)
-        if kern:
+        if kern and K == 4096:
             traffic = kern["hbm_bytes_per_frame_per_launch"] * tm["reduce_frames"]
     metric = "encoded Msamples/s @44.1kHz stereo ChunkSize=8 ChunkCount=4096; bit-exact .gsc"  # BASELINE.json
     if args.config != "c2":
         metric = f"encoded Msamples/s ({desc}); bit-exact .gsc"
-    result = {
+    return {
         "metric": metric,
         "value": round(value, 4),
         "unit": "Msamples/s",
@@ -209,37 +311,86 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(dt * 1e3 / args.steps, 2),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": f"synthetic (SURVEY.md §8d tone+noise, PCG64 20250217), {args.seconds:g} s per GPU",
-        "config": {"workload": f"{desc}, {total_seconds:g} s synthetic", "frames": nframes, "argv": argv,
-                   "parallelism": f"frame-sharded x{ws}", "rank0_frames": [b, e]},
-        "prepare_ms": round(prep.prepare_ms, 1),
-        "realtime_x": round(value / (rate * ch / 1e6), 2),
         "roofline": {"bound": "valu", "kernel": "scan_batch_kernel", "achieved": round(achieved, 4),
-                     "peak": VALU_F32_PEAK_TOPS, "unit": "Tops/s (algorithmic: the reference's sub+mul+add per leaf coordinate, 6K ops per sample per "
-                             "pass; peak = non-fused f32 VALU issue rate; the kernel itself bounds distances with one "
-                             "fma per coordinate and recomputes exactly only what it commits)",
+                     "peak": VALU_F32_PEAK_TOPS,
+                     "unit": "Tops/s (algorithmic: the reference's sub+mul+add per leaf coordinate, 6K ops per "
+                             "sample per pass; peak = non-fused f32 VALU issue rate; the kernel itself bounds "
+                             "distances with one fma per coordinate and recomputes exactly only what it commits)",
                      "frac": round(achieved / VALU_F32_PEAK_TOPS, 5),
                      "traffic": None if traffic is None else round(traffic),
-                     "hbm_gbs": None if traffic is None else round(traffic / avg_launch_s / 1e9, 2),
-                     "hbm_frac": None if traffic is None else round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 6),
+                     "hbm_gbs": None if traffic is None or avg_launch_s <= 0 else round(traffic / avg_launch_s / 1e9, 2),
+                     "hbm_frac": None if traffic is None or avg_launch_s <= 0 else
+                     round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 6),
                      "avg_launch_ms": round(avg_launch_s * 1e3, 3), "ops_per_launch": ops / launches},
         # host_post_ms: what the KNNFit / prune / packing pipeline adds after the
         # scan; post_overlap_ms: the part of it that ran in the scan tail
-        "stages_ms": {k: round(tm[k], 1) for k in ("host_prepare_ms", "host_frames_ms", "gpu_dsp_ms", "gpu_yakmo_ms",
-                                                    "gpu_scan_ms", "gpu_knnfit_ms", "host_post_ms", "post_overlap_ms",
-                                                    "total_ms")},
+        "stages_ms": {k: round(tm[k], 1) for k in ("host_frames_ms", "gpu_dsp_ms", "gpu_yakmo_ms", "gpu_scan_ms",
+                                                    "gpu_knnfit_ms", "host_post_ms", "post_overlap_ms", "total_ms")},
         "post_groups": tm["post_groups"],
-        "stages_note": ("host_frames, gpu_dsp, gpu_yakmo, gpu_scan and host_post run in series; gpu_knnfit_ms is "
-                        "submit-to-done of the KNNFit groups, which run on the CUs of finished frames during the "
-                        "scan tail (post_overlap_ms), so it is not additive"),
+        "stages_note": ("stages of rank 0's last encode: host_frames, gpu_dsp, gpu_yakmo, gpu_scan and host_post run "
+                        "in series; gpu_knnfit_ms is submit-to-done of the KNNFit groups, which run on the CUs of "
+                        "finished frames during the scan tail (post_overlap_ms), so it is not additive; PrepareFrames "
+                        "(prepare_ms) overlaps the previous job's encode"),
         "scan": {"passes": tm["scan_passes"], "searches": tm["scan_point_passes"], "exact_dfs": tm["scan_slow"],
                  "solo_resolutions": tm["scan_restarts"]},
     }
+
+
+def bench_corpus(args, enc, argv, desc, ws, rank, local, dist):
+    """configs[3]: the 22-file lame_test corpus as ONE batch -- every frame of
+    every file in one device launch per stage (gsc_encode_many), frames of the
+    batch sharded across ranks by chunk count, one .gsc per file on rank 0."""
+    import torch
+
+    import soundchunks_amd as sc
+
+    names = sorted(n for n in os.listdir(CORPUS) if n.endswith(".wav"))
+    wavs = [(CORPUS / n).read_bytes() for n in names]
+    dev = torch.device("cuda", local)
+
+    def step():
+        return sc.encode_many(wavs, argv, rank=rank, world_size=ws, device=dev if dist is not None else None)
+
+    lat = None
+    for w in range(args.warmup):
+        t = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        if w == 0:
+            lat = (time.perf_counter() - t) * 1e3
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        outs = step()
+    tm = sc.Encoder.last_timing()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    n_samples = sum((len(w) - 44) // 2 for w in wavs)
+    value = n_samples * args.steps / dt / 1e6
+    result = base_result(args, ws, dt, value, desc, enc, tm, 8, argv, 44100, 1)
+    result["config"] = {"workload": f"{desc}, {n_samples / 44100:.1f} s of audio in {len(wavs)} files",
+                        "files": len(wavs), "frames": tm["frames"], "argv": argv,
+                        "parallelism": f"frame-sharded x{ws}"}
+    result["data"] = "the reference's lame_test corpus WAVs (tests/golden/lame_test), encoded as one batch"
+    result["job_latency_ms"] = None if lat is None else round(lat, 1)
+    result["realtime_x"] = round(value / (44100 / 1e6), 2)
+    result["outputs_bytes"] = sum(len(o) for o in outs)
     if not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(argv, rate, ch, enc.frame_length / 1000.0, args.cpu_threads)
+        result["cpu_baseline"] = cpu_baseline("c4", argv, 44100, 1, enc.frame_length / 1000.0, args.cpu_threads)
     print(json.dumps(result))
     if dist is not None:
         dist.destroy_process_group()

@@ -118,7 +118,34 @@ int gsc_prepared_frame_count(const gsc_prepared *p);
 int gsc_prepared_frame_chunks(const gsc_prepared *p, int *chunks);
 int gsc_encode_prepared(gsc_prepared *p, int frame_begin, int frame_end, uint8_t **out, size_t *out_len);
 double gsc_prepared_prepare_ms(const gsc_prepared *p);
+/* The frame boundaries PrepareFrames chose: sample index of every frame's
+ * first and last sample (gsc_prepared_frame_count entries each). */
+int gsc_prepared_frame_bounds(const gsc_prepared *p, int *starts, int *ends);
+/* A prepared encoder over boundaries computed elsewhere (one rank runs
+ * PrepareFrames on the whole file and broadcasts them): no power scans, and
+ * only the samples of frames [frame_begin, frame_end) are loaded, so only
+ * that range may be encoded.  frame_end = -1: up to frame_count.  The bounds
+ * must be contiguous, block-aligned and cover the file (else NULL). */
+gsc_prepared *gsc_prepare_frames(const uint8_t *wav, size_t wav_len, const gsc_options *o, const int *starts,
+                                 const int *ends, int frame_count, int frame_begin, int frame_end);
 void gsc_prepared_free(gsc_prepared *p);
+
+/* Batch of WAVs as one job (the reference encodes a corpus file by file;
+ * encoder.lpr:1431-1451 runs each file's frames on its thread pool): every
+ * file gets its own Load + PrepareFrames, then the frames of ALL files form
+ * one frame list, so every stage runs one device launch for the whole batch.
+ * The files must share channel count, sample rate and the resulting
+ * ChunksPerFrame.  gsc_prepared_file_frames writes file_count + 1 entries: the
+ * first frame of every file, then the total.  gsc_encode_prepared_files
+ * encodes frames [frame_begin, frame_end) of the list and also writes, per
+ * file, how many of the returned bytes belong to it (files in order; a file's
+ * .gsc is its bytes from every range, in range order). */
+gsc_prepared *gsc_prepare_many(const uint8_t *const *wavs, const size_t *wav_lens, int file_count,
+                               const gsc_options *o);
+int gsc_prepared_file_count(const gsc_prepared *p);
+int gsc_prepared_file_frames(const gsc_prepared *p, int *first_frame);
+int gsc_encode_prepared_files(gsc_prepared *p, int frame_begin, int frame_end, uint8_t **out, size_t *out_len,
+                              size_t *file_bytes);
 
 /* Device DSP of one frame (FindAttenuationDivider, encoder.lpr:566-605, and the
  * MakeChunks features, encoder.lpr:467-485): *feat = n_chunks x 2*ChunkSize

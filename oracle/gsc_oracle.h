@@ -119,6 +119,7 @@ typedef struct {
     float knn_eps;
 } ora_frame_trace;
 /* Fills the trace (caller frees arrays with ora_free). Returns 0 on success. */
+int ora_frame_bounds(const uint8_t *wav, size_t wav_len, const gsc_params *p, int *starts, int *ends, int cap);
 int ora_trace_frame(const uint8_t *wav, size_t wav_len, const gsc_params *p, int frame_idx,
                     ora_frame_trace *tr);
 

@@ -94,6 +94,15 @@ SIGNATURES = {
     "gsc_prepare": (ctypes.c_void_p, [_U8P, ctypes.c_size_t, ctypes.POINTER(GscOptions)]),
     "gsc_prepared_frame_count": (ctypes.c_int, [ctypes.c_void_p]),
     "gsc_prepared_frame_chunks": (ctypes.c_int, [ctypes.c_void_p, _IP]),
+    "gsc_prepared_frame_bounds": (ctypes.c_int, [ctypes.c_void_p, _IP, _IP]),
+    "gsc_prepare_frames": (ctypes.c_void_p, [_U8P, ctypes.c_size_t, ctypes.POINTER(GscOptions), _IP, _IP, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_int]),
+    "gsc_prepare_many": (ctypes.c_void_p, [ctypes.POINTER(_U8P), ctypes.POINTER(ctypes.c_size_t), ctypes.c_int,
+                                           ctypes.POINTER(GscOptions)]),
+    "gsc_prepared_file_count": (ctypes.c_int, [ctypes.c_void_p]),
+    "gsc_prepared_file_frames": (ctypes.c_int, [ctypes.c_void_p, _IP]),
+    "gsc_encode_prepared_files": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_U8P),
+                                                 ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]),
     "gsc_encode_prepared": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_U8P),
                                            ctypes.POINTER(ctypes.c_size_t)]),
     "gsc_prepared_prepare_ms": (ctypes.c_double, [ctypes.c_void_p]),

@@ -3,10 +3,14 @@
 #include "gsc_encoder.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "fpc_math.h"
+#include "gsc_seqsum.h"
 
 namespace gsc {
 namespace {
@@ -142,8 +146,11 @@ void trig_pack(int cs, std::vector<double>* tab, double* s0, double* scale) {
     *scale = std::sqrt(2.0 / double(cs));
 }
 
-// TEncoder.Load + PrepareFrames (encoder.lpr:1111-1152, 1241-1273, 1294-1429)
-int Encoder::prepare(const uint8_t* wav, size_t len, std::string* err) {
+// TEncoder.Load (encoder.lpr:1111-1152) and the option / geometry part of
+// PrepareFrames (encoder.lpr:1241-1351): header, SampleCount padded to whole
+// blocks, the -br ChunksPerFrame search.  The SmallInt samples of [s0, s1)
+// (zero past the file's end) are copied into pcm_.
+int Encoder::load(const uint8_t* wav, size_t len, int64_t s0, int64_t s1, std::string* err) {
     if (len < 44) {
         *err = "WAV shorter than its 44-byte header";
         return -1;
@@ -169,7 +176,12 @@ int Encoder::prepare(const uint8_t* wav, size_t len, std::string* err) {
         return -2;
     }
     const int cs = o.chunk_size, ch = channels_;
-    const int sc = int((len - 44) / (2 * size_t(ch)));
+    const int64_t sc64 = int64_t((len - 44) / (2 * size_t(ch)));
+    if (sc64 > int64_t(INT32_MAX) / 2) {
+        *err = "sample count out of range";
+        return -1;
+    }
+    const int sc = int(sc64);
     const double hc = std::min(o.high_cut, double(sample_rate_) / 2);
     const double fcl = o.low_cut / double(sample_rate_), fch = hc / double(sample_rate_);
     if (fcl > 0.0 || fch < 0.5) {
@@ -179,35 +191,12 @@ int Encoder::prepare(const uint8_t* wav, size_t len, std::string* err) {
     const int under = int(std::max<int64_t>(1, fpc::round(0.25 / fch)));
     block_ = under * (cs - o.chunk_blend);
     sample_count_ = ((sc - 1) / block_ + 1) * block_;  // Pascal div truncates
+    file_samples_ = sc;
     const int SC = sample_count_;
-    filtered_.resize(size_t(ch));
-    for (auto& v : filtered_) v.resize(size_t(std::max(SC, 1)));  // no fill: the workers below write every sample
-    pcm_.resize(size_t(std::max(SC, 1)) * size_t(ch));
-    const uint8_t* d = wav + 44;
-    // per-sample work in parallel blocks; every sequential f64 sum below keeps
-    // the reference's order (encoder.lpr:1374-1425)
-    constexpr int kBlk = 1 << 16;
-    const int nblk = (std::max({SC, sc, 1}) + kBlk - 1) / kBlk;
-    parallel_for(nblk, host_threads(), [&](int k) {
-        const int i1 = std::min(sc, (k + 1) * kBlk);
-        for (int i = k * kBlk; i < i1; ++i)
-            for (int c = 0; c < ch; ++c) {
-                const uint8_t* b = d + (size_t(i) * ch + c) * 2;
-                const int16_t v = int16_t(uint16_t(b[0] | (b[1] << 8)));
-                pcm_[size_t(i) * ch + c] = v;
-                filtered_[c][i] = double(v) / 32767.0;
-            }
-        const int z1 = std::min(std::max(SC, 1), (k + 1) * kBlk);  // zero padding past the WAV end
-        for (int i = std::max(sc, k * kBlk); i < z1; ++i)
-            for (int c = 0; c < ch; ++c) {
-                pcm_[size_t(i) * ch + c] = 0;
-                filtered_[c][i] = 0.0;
-            }
-    });
-    const int frame_count = int(fpc::ceil_pos(double(SC) / (double(sample_rate_) * (o.frame_length / 1000.0))));
+    frame_count_est_ = int(fpc::ceil_pos(double(SC) / (double(sample_rate_) * (o.frame_length / 1000.0))));
     // ChunksPerFrame search only changes anything with -br (encoder.lpr:1337-1351)
-    int cpf = o.chunks_per_frame;
     if (o.bit_rate > 0) {
+        int cpf = o.chunks_per_frame;
         const long long projected =
             (long long)std::ceil((double(SC) / double(sample_rate_)) * (double(o.bit_rate) * 1024.0 / 8.0));
         ++cpf;
@@ -216,47 +205,279 @@ int Encoder::prepare(const uint8_t* wav, size_t len, std::string* err) {
             const double band = (double(SC) * double(ch) * (std::log2(double(cpf)) + 3 + 1 + 1)) /
                                 (8.0 * double(cs - o.chunk_blend) * double(under));
             const double frame = double(cpf * cs) * double(o.chunk_bit_depth) / 8.0 + double(cpf) * 4.0 / 8.0 + 16;
-            const int32_t tent = int32_t(fpc::round(0.0 + band * 0.8 + double(frame_count) * frame));
+            const int32_t tent = int32_t(fpc::round(0.0 + band * 0.8 + double(frame_count_est_) * frame));
             if (tent <= projected || cpf <= 1) break;
         }
         opt_.chunks_per_frame = cpf;
     }
-    // pass 2: RMS-power balanced frame boundaries, sequential f64 (encoder.lpr:1374-1425)
-    double avg = 0.0;
-    for (int j = 0; j < ch; ++j) {
-        const double* f = filtered_[j].data();
-        for (int i = 0; i < SC; ++i) avg += f[i] * f[i];
-    }
-    avg = std::sqrt(avg / double(SC * ch));
-    std::vector<double> pw(static_cast<size_t>(std::max(SC, 1)));
+    // the samples of [s0, s1): a straight copy of the little-endian PCM16
+    // (zero past the file, PrepareFrames pads SampleCount, encoder.lpr:1317-1323)
+    s0 = std::max<int64_t>(0, s0);
+    s1 = std::min<int64_t>(SC, s1);
+    pcm_off_ = s0;
+    const int64_t n = std::max<int64_t>(s1 - s0, 1);
+    pcm_.resize(size_t(n) * size_t(ch));
+    const int64_t have = std::max<int64_t>(0, std::min<int64_t>(s1, sc) - s0);
+    constexpr int64_t kBlk = int64_t(1) << 18;
+    const int nblk = int((n + kBlk - 1) / kBlk);
+    const uint8_t* d = wav + 44;
     parallel_for(nblk, host_threads(), [&](int k) {
-        const int i1 = std::min(SC, (k + 1) * kBlk);
-        for (int i = k * kBlk; i < i1; ++i) {
-            double s = 0.0;
-            for (int j = 0; j < ch; ++j) s += filtered_[j][i] * filtered_[j][i];
-            s = std::sqrt(s / double(ch));
-            pw[i] = 1.0 - (avg + (s - avg) * o.vfr);
-        }
+        const int64_t a = int64_t(k) * kBlk, b = std::min(n, a + kBlk);
+        const int64_t c = std::min(b, have);
+        if (c > a) std::memcpy(pcm_.data() + size_t(a) * ch, d + size_t(s0 + a) * ch * 2, size_t(c - a) * ch * 2);
+        if (b > std::max(a, c))
+            std::memset(pcm_.data() + size_t(std::max(a, c)) * ch, 0, size_t(b - std::max(a, c)) * ch * 2);
     });
-    double total = 0.0;
-    for (int i = 0; i < SC; ++i) total += pw[i];
-    const double per_frame = total / double(frame_count);
+    return 0;
+}
+
+// PrepareFrames pass 2 (encoder.lpr:1374-1425): avgPower, totalPower and the
+// RMS-power balanced frame cut, every f64 sum bit-identical to the
+// reference's sequential loops -- evaluated in parallel (gsc_seqsum.h) and,
+// for the cut, by speculating the frame boundaries from an approximate
+// prefix and verifying every frame's exact running sum.
+int Encoder::plan(std::string* err) {
+    const int SC = sample_count_, ch = channels_;
+    if (pcm_off_ != 0 || int64_t(pcm_.size()) < int64_t(SC) * ch) {
+        *err = "PrepareFrames needs the whole file loaded";
+        return -1;
+    }
+    const int16_t* pcm = pcm_.data();
+    const int T = host_threads();
+    const bool tm = std::getenv("GSC_HOST_TIMING") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    const auto q0 = now();
+    SeqSumStats st_avg, st_tot;
+    auto par = [&](int n, const std::function<void(int)>& fn) { parallel_for(n, T, fn); };
+    // Sqr(makeFloatSample(srcData)) per SmallInt value, srcData = s / 32767
+    static const std::vector<double> sq = [] {
+        std::vector<double> t(65536);
+        for (int v = -32768; v < 32768; ++v) {
+            const double f = double(v) / 32767.0;
+            t[size_t(v + 32768)] = f * f;
+        }
+        return t;
+    }();
+    const double* SQ = sq.data() + 32768;
+    // avgPower: channel-major sum over the padded SampleCount
+    const int64_t nn = int64_t(SC) * ch;
+    double avg = exact_seq_sum(
+        nn, 0.0,
+        [&](int64_t a, int64_t b, double* o) {
+            int64_t j = a / SC, i = a - j * SC;
+            for (int64_t k = a; k < b; ++k) {
+                *o++ = SQ[pcm[size_t(i) * ch + size_t(j)]];
+                if (++i == SC) {
+                    i = 0;
+                    ++j;
+                }
+            }
+        },
+        par, 8192, tm ? &st_avg : nullptr);
+    avg = std::sqrt(avg / double(SC * ch));
+    const auto q1 = now();
+    // 1 - lerp(avgPower, smp, VariableFrameSizeRatio) per sample
+    const double vfr = opt_.vfr;
+    auto pw_of = [&](int64_t i) {
+        double sm = 0.0;
+        for (int j = 0; j < ch; ++j) sm += SQ[pcm[size_t(i) * ch + j]];
+        sm = std::sqrt(sm / double(ch));
+        return 1.0 - (avg + (sm - avg) * vfr);
+    };
+    std::vector<double, NoInitAlloc<double>> pw(static_cast<size_t>(SC));
+    double* PW = pw.data();
+    const double total = exact_seq_sum(
+        SC, 0.0,
+        [&](int64_t a, int64_t b, double* o) {  // pw is materialised on the way (the cut reads it)
+            for (int64_t i = a; i < b; ++i) o[i - a] = PW[i] = pw_of(i);
+        },
+        par, 8192, tm ? &st_tot : nullptr);
+    const double* P = PW;
+    const auto q2 = now();
+    const double per_frame = total / double(frame_count_est_);
+    const auto q3 = now();
+    // the cut: cur += pw[i]; at block-aligned i with cur >= perFramePower a frame
+    // ends at i - 1 and cur restarts at 0 (pw[i] itself is not carried over)
+    cut_frames(P, per_frame);
+    if (tm)
+        std::fprintf(stderr,
+                     "plan [ms]: avg %.1f pw+total %.1f cut %.1f | exact sums: avg %lld/%lld blocks on the grid "
+                     "(%lld ties), total %lld/%lld (%lld ties)\n",
+                     ms(q0, q1), ms(q1, q2), ms(q3, now()), (long long)st_avg.fast_blocks, (long long)st_avg.blocks,
+                     (long long)st_avg.ties, (long long)st_tot.fast_blocks, (long long)st_tot.blocks,
+                     (long long)st_tot.ties);
+    return 0;
+}
+
+void Encoder::cut_frames(const double* P, double per_frame) {
+    const int SC = sample_count_, B = block_;
+    // approximate prefix by 4096-sample blocks (speculation only)
+    constexpr int kB = 4096;
+    const int nb = (SC + kB - 1) / kB;
+    std::vector<double> bsum(static_cast<size_t>(nb));
+    parallel_for(nb, host_threads(), [&](int b) {
+        double a = 0.0;
+        const int i1 = std::min(SC, (b + 1) * kB);
+        for (int i = b * kB; i < i1; ++i) a += P[i];
+        bsum[size_t(b)] = a;
+    });
+    // approximate end of the frame whose running sum starts after `s` (frame 0: at 0)
+    auto spec_end = [&](int first) -> int {  // first = first index added to cur
+        double cur = 0.0;
+        int i = first;
+        while (i < SC) {
+            const int b = i / kB;
+            // skip whole blocks that cannot reach the threshold, even with +-1e-6 slack
+            if (i == b * kB && b + 1 < nb && cur + bsum[size_t(b)] < per_frame * (1.0 - 1e-6) - 1e-6) {
+                cur += bsum[size_t(b)];
+                i = (b + 1) * kB;
+                continue;
+            }
+            cur += P[i];
+            if (i % B == 0 && cur >= per_frame) return i;
+            ++i;
+        }
+        return SC;  // no cut: the last frame
+    };
+    // exact end (the reference's loop) of the frame whose sum starts at `first`
+    auto exact_end = [&](int first) -> int {
+        double cur = 0.0;
+        for (int i = first; i < SC; ++i) {
+            cur += P[i];
+            if (i % B == 0 && cur >= per_frame) return i;
+        }
+        return SC;
+    };
+    std::vector<int> cuts;  // exact cut indices (frame k + 1 starts at cuts[k])
+    int first = 0;          // frame 0 sums from 0, later frames from cut + 1
+    for (;;) {
+        // speculate the remaining cuts, then verify every frame's exact sum in parallel
+        std::vector<int> spec;
+        for (int f = first; f < SC;) {
+            const int c = spec_end(f);
+            if (c >= SC) break;
+            spec.push_back(c);
+            f = c + 1;
+        }
+        const int ns = int(spec.size());
+        std::vector<int> exact(static_cast<size_t>(ns) + 1);
+        parallel_for(ns + 1, host_threads(), [&](int k) {
+            const int f = k == 0 ? first : spec[size_t(k - 1)] + 1;
+            exact[size_t(k)] = f < SC ? exact_end(f) : SC;
+        });
+        int k = 0;
+        while (k < ns && exact[size_t(k)] == spec[size_t(k)]) cuts.push_back(spec[size_t(k++)]);
+        if (k == ns && exact[size_t(ns)] >= SC) break;  // every speculated frame verified, the last runs to the end
+        // first mismatch: frame k's exact cut, then speculate again after it
+        if (exact[size_t(k)] >= SC) break;
+        cuts.push_back(exact[size_t(k)]);
+        first = exact[size_t(k)] + 1;
+        if (first >= SC) break;
+    }
     fr_start_.clear();
     fr_end_.clear();
     int next = 0;
-    double cur = 0.0;
-    for (int i = 0, r = 0; i < SC; ++i, r = (r + 1 == block_) ? 0 : r + 1) {  // r = i mod block_
-        cur += pw[i];
-        if ((r == 0) && (cur >= per_frame)) {
-            fr_start_.push_back(next);
-            fr_end_.push_back(i - 1);
-            cur = 0.0;
-            next = i;
-        }
+    for (int c : cuts) {
+        fr_start_.push_back(next);
+        fr_end_.push_back(c - 1);
+        next = c;
     }
     fr_start_.push_back(next);
     fr_end_.push_back(SC - 1);
+}
+
+// TEncoder.Load + PrepareFrames (encoder.lpr:1111-1152, 1241-1273, 1294-1429)
+int Encoder::prepare(const uint8_t* wav, size_t len, std::string* err) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = load(wav, len, 0, INT64_MAX, err);
+    if (rc != 0) return rc;
+    const auto t1 = std::chrono::steady_clock::now();
+    const int r2 = plan(err);
+    if (std::getenv("GSC_HOST_TIMING")) {
+        const auto t2 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "prepare [ms]: load %.1f plan %.1f (%d threads)\n",
+                     std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                     std::chrono::duration<double, std::milli>(t2 - t1).count(), host_threads());
+    }
+    return r2;
+}
+
+int Encoder::prepare_many(const uint8_t* const* wavs, const size_t* lens, int nfiles, std::string* err) {
+    if (nfiles <= 0) {
+        *err = "prepare_many: no files";
+        return -1;
+    }
+    std::vector<Encoder> es(static_cast<size_t>(nfiles), Encoder(opt_));
+    for (int f = 0; f < nfiles; ++f) {
+        const int rc = es[size_t(f)].prepare(wavs[f], lens[f], err);
+        if (rc != 0) {
+            *err = "file " + std::to_string(f) + ": " + *err;
+            return rc;
+        }
+        const Encoder& a = es[size_t(f)];
+        const Encoder& z = es[0];
+        if (a.channels_ != z.channels_ || a.sample_rate_ != z.sample_rate_ ||
+            a.opt_.chunks_per_frame != z.opt_.chunks_per_frame) {
+            *err = "prepare_many: a batch needs one channel count, sample rate and ChunksPerFrame (file " +
+                   std::to_string(f) + " differs)";
+            return -2;
+        }
+    }
+    *this = Encoder(es[0].opt_);
+    channels_ = es[0].channels_;
+    sample_rate_ = es[0].sample_rate_;
+    block_ = es[0].block_;
+    int64_t total = 0;
+    for (const Encoder& a : es) total += a.sample_count_;
+    if (total > INT32_MAX / 2) {
+        *err = "prepare_many: batch too long";
+        return -1;
+    }
+    sample_count_ = int(total);
+    file_samples_ = sample_count_;
+    pcm_off_ = 0;
+    pcm_.resize(size_t(std::max<int64_t>(total, 1)) * size_t(channels_));
+    file_first_.assign(1, 0);
+    int64_t base = 0;
+    for (const Encoder& a : es) {
+        std::memcpy(pcm_.data() + size_t(base) * channels_, a.pcm_.data(), size_t(a.sample_count_) * channels_ * 2);
+        for (size_t k = 0; k < a.fr_start_.size(); ++k) {
+            fr_start_.push_back(int(base + a.fr_start_[k]));
+            fr_end_.push_back(int(base + a.fr_end_[k]));
+        }
+        file_first_.push_back(int(fr_start_.size()));
+        base += a.sample_count_;
+    }
     return 0;
+}
+
+// an encoder over frame boundaries computed elsewhere (rank 0's PrepareFrames,
+// multi-GPU sharding): the geometry of load(), then only the samples of frames
+// [b, e) are copied
+int Encoder::prepare_bounds(const uint8_t* wav, size_t len, const int* starts, const int* ends, int nframes, int b,
+                            int e, std::string* err) {
+    if (nframes <= 0 || b < 0 || e > nframes || b > e) {
+        *err = "frame bounds: invalid frame range";
+        return -1;
+    }
+    // geometry first (no samples), then validate the bounds against it
+    int rc = load(wav, len, 0, 0, err);
+    if (rc != 0) return rc;
+    const int SC = sample_count_;
+    if (starts[0] != 0 || ends[nframes - 1] != SC - 1) {
+        *err = "frame bounds do not cover the file";
+        return -1;
+    }
+    for (int i = 0; i < nframes; ++i)
+        if (ends[i] < starts[i] || (i > 0 && starts[i] != ends[i - 1] + 1) || starts[i] % block_ != 0) {
+            *err = "frame bounds are not contiguous block-aligned frames";
+            return -1;
+        }
+    fr_start_.assign(starts, starts + nframes);
+    fr_end_.assign(ends, ends + nframes);
+    if (e > b) rc = load(wav, len, starts[b], int64_t(ends[e - 1]) + 1, err);
+    return rc;
 }
 
 // MakeChunks srcData (encoder.lpr:467-485): chunk-major, channel-minor, zero
@@ -276,10 +497,10 @@ void Encoder::frame_host_src(FrameState& f) const {
 void Encoder::chunk_src(const FrameState& f, int j, double* out) const {
     const int cs = opt_.chunk_size, ch = channels_;
     const int i = j / ch, c = j - i * ch;
-    const double* row = filtered_[size_t(c)].data() + f.start;
+    const int16_t* base = pcm_.data() + (size_t(int64_t(f.start) - pcm_off_) * ch + size_t(c));
     for (int k = 0; k < cs; ++k) {
         const int pos = i * cs + k;
-        out[k] = pos >= f.sample_count ? 0.0 : 0.0 + row[pos];
+        out[k] = pos >= f.sample_count ? 0.0 : 0.0 + double(base[size_t(pos) * ch]) / 32767.0;  // srcData = s / 32767
     }
 }
 

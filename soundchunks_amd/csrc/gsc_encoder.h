@@ -98,6 +98,17 @@ class Encoder {
     explicit Encoder(const gsc_options& o) : opt_(o) {}
     // Load + PrepareFrames; returns 0 or a negative error code
     int prepare(const uint8_t* wav, size_t len, std::string* err);
+    // frame boundaries computed elsewhere (starts/ends of all nframes frames);
+    // only the samples of frames [b, e) are loaded
+    int prepare_bounds(const uint8_t* wav, size_t len, const int* starts, const int* ends, int nframes, int b, int e,
+                       std::string* err);
+    const std::vector<int>& frame_starts() const { return fr_start_; }
+    const std::vector<int>& frame_ends() const { return fr_end_; }
+    // a batch of WAVs (same channel count, sample rate and ChunksPerFrame) as
+    // one frame list: each file's own Load + PrepareFrames, the files' padded
+    // samples back to back, frames of file f from file_first()[f]
+    int prepare_many(const uint8_t* const* wavs, const size_t* lens, int nfiles, std::string* err);
+    const std::vector<int>& file_first() const { return file_first_; }
     int frame_count() const { return int(fr_start_.size()); }
     // chunkRefs count of frame i: chunks x channels (encoder.lpr:467-485)
     int frame_chunks(int i) const {
@@ -106,7 +117,7 @@ class Encoder {
     }
     // Encode frames [b, e) and return their concatenated stream bytes
     int encode_range(int b, int e, std::vector<uint8_t>* out, std::string* err, gsc_timing* tim,
-                     ReconOut* recon = nullptr);
+                     ReconOut* recon = nullptr, std::vector<size_t>* frame_bytes = nullptr);
     // Device DSP of frame f alone (parity tests): attenuation divider and the
     // N x 2CS features
     int dsp_frame(int f, int* atten_div, std::vector<float>* feat, std::string* err);
@@ -116,6 +127,11 @@ class Encoder {
     long long sample_count() const { return sample_count_; }
 
    private:
+    // Load: header, geometry, the samples of [s0, s1) into pcm_
+    int load(const uint8_t* wav, size_t len, int64_t s0, int64_t s1, std::string* err);
+    // PrepareFrames pass 2: power sums and the frame cut (needs the whole file loaded)
+    int plan(std::string* err);
+    void cut_frames(const double* pw, double per_frame);
     void frame_host_src(FrameState& f) const;  // chunk count (encoder.lpr:467-485)
     void chunk_src(const FrameState& f, int j, double* out) const;  // chunk j's srcData (CS doubles)
     // device DSP for frames (first frame index b): atten_div, neg / rev on the
@@ -137,11 +153,14 @@ class Encoder {
 
     gsc_options opt_;
     int channels_ = 0, sample_rate_ = 0;
-    int sample_count_ = 0;
+    int sample_count_ = 0;   // SampleCount, padded to whole blocks
+    int file_samples_ = 0;   // sample frames in the WAV
+    int frame_count_est_ = 0;  // FrameCount before the cut (encoder.lpr:1335)
     int block_ = 1;
-    std::vector<std::vector<double, NoInitAlloc<double>>> filtered_;  // [ch][sample] = s / 32767
-    std::vector<int16_t, NoInitAlloc<int16_t>> pcm_;                  // [sample][ch] SmallInt, zero padded (device upload)
+    int64_t pcm_off_ = 0;    // first sample held in pcm_
+    std::vector<int16_t, NoInitAlloc<int16_t>> pcm_;  // [sample - pcm_off_][ch] SmallInt, zero padded (srcData * 32767)
     std::vector<int> fr_start_, fr_end_;
+    std::vector<int> file_first_{0};  // first frame of each file (+ the total), one file unless prepare_many
 };
 
 }  // namespace gsc

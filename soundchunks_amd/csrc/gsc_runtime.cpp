@@ -657,7 +657,7 @@ int Encoder::device_dsp(int b, std::vector<FrameState>& frames, void* dXv, std::
         return false;
     };
     // the SmallInt samples of the span (a quarter of the f64 bytes), converted on the device
-    if (!chk(hipMemcpy(dP.p, pcm_.data() + size_t(s_first) * ch, sizeof(int16_t) * size_t(ch) * size_t(span),
+    if (!chk(hipMemcpy(dP.p, pcm_.data() + size_t(s_first - pcm_off_) * ch, sizeof(int16_t) * size_t(ch) * size_t(span),
                        hipMemcpyHostToDevice),
              "sample upload") ||
         !chk(gsc_launch_pcm(dP.p, span, ch, dS.p, nullptr), "sample conversion"))
@@ -975,7 +975,7 @@ int Encoder::dsp_frame(int fi, int* atten_div, std::vector<float>* feat, std::st
 
 // ---- Encoder::encode_range: host srcData, device DSP + hot path ------------
 int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* err, gsc_timing* tim,
-                          ReconOut* recon) {
+                          ReconOut* recon, std::vector<size_t>* frame_bytes) {
     if (ensure_device() != 0) {
         *err = t_err;
         return -1;
@@ -1195,6 +1195,10 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
     for (auto& f : frames) bytes += f.stream.size();
     out->reserve(bytes);
     for (auto& f : frames) out->insert(out->end(), f.stream.begin(), f.stream.end());
+    if (frame_bytes) {
+        frame_bytes->clear();
+        for (auto& f : frames) frame_bytes->push_back(f.stream.size());
+    }
     double t4 = now_ms();
     if (std::getenv("GSC_HOST_TIMING"))
         std::fprintf(stderr,
@@ -1311,15 +1315,26 @@ int gsc_count_frames(const uint8_t* wav, size_t wav_len, const gsc_options* o, i
 
 // encode frames [frame_begin, frame_end) of a prepared encoder into a
 // library-allocated buffer; timing lands in t_tim (host_prepare_ms excluded)
-static int encode_prepared(Encoder& enc, int frame_begin, int frame_end, uint8_t** out, size_t* out_len) {
+static int encode_prepared(Encoder& enc, int frame_begin, int frame_end, uint8_t** out, size_t* out_len,
+                           size_t* file_bytes = nullptr) {
     const double t0 = now_ms();
     const int fc = enc.frame_count();
     frame_begin = std::max(0, frame_begin);
     frame_end = std::min(fc, frame_end < 0 ? fc : frame_end);
     std::vector<uint8_t> bytes;
+    std::vector<size_t> fb;
     std::string err;
     if (frame_end > frame_begin) {
-        if (enc.encode_range(frame_begin, frame_end, &bytes, &err, &t_tim) != 0) return fail(err);
+        if (enc.encode_range(frame_begin, frame_end, &bytes, &err, &t_tim, nullptr, &fb) != 0) return fail(err);
+    }
+    if (file_bytes) {  // the range's bytes of every file of the batch
+        const std::vector<int>& ff = enc.file_first();
+        for (size_t f = 0; f + 1 < ff.size(); ++f) {
+            size_t n = 0;
+            for (int i = std::max(ff[f], frame_begin); i < std::min(ff[f + 1], frame_end); ++i)
+                n += fb[size_t(i - frame_begin)];
+            file_bytes[f] = n;
+        }
     }
     *out = static_cast<uint8_t*>(std::malloc(std::max<size_t>(bytes.size(), 1)));
     if (!*out) return fail("out of host memory");
@@ -1351,6 +1366,7 @@ int gsc_encode_wav_frames(const uint8_t* wav, size_t wav_len, const gsc_options*
 struct gsc_prepared {
     Encoder enc;
     double prepare_ms = 0;
+    int loaded_begin = 0, loaded_end = -1;  // frames whose samples are held (-1: all)
     explicit gsc_prepared(const gsc_options& o) : enc(o) {}
 };
 
@@ -1385,8 +1401,47 @@ int gsc_prepared_frame_chunks(const gsc_prepared* p, int* chunks) {
     return 0;
 }
 
+int gsc_prepared_frame_bounds(const gsc_prepared* p, int* starts, int* ends) {
+    if (!p || !starts || !ends) return fail("gsc_prepared_frame_bounds: null argument");
+    const auto& s = p->enc.frame_starts();
+    const auto& e = p->enc.frame_ends();
+    std::copy(s.begin(), s.end(), starts);
+    std::copy(e.begin(), e.end(), ends);
+    return 0;
+}
+
+gsc_prepared* gsc_prepare_frames(const uint8_t* wav, size_t wav_len, const gsc_options* o, const int* starts,
+                                 const int* ends, int frame_count, int frame_begin, int frame_end) {
+    if (!wav || !o || !starts || !ends) {
+        fail("gsc_prepare_frames: null argument");
+        return nullptr;
+    }
+    const double t0 = now_ms();
+    gsc_prepared* p = new (std::nothrow) gsc_prepared(*o);
+    if (!p) {
+        fail("gsc_prepare_frames: out of host memory");
+        return nullptr;
+    }
+    std::string err;
+    if (frame_end < 0) frame_end = frame_count;
+    if (p->enc.prepare_bounds(wav, wav_len, starts, ends, frame_count, frame_begin, frame_end, &err) != 0) {
+        delete p;
+        fail(err);
+        return nullptr;
+    }
+    p->loaded_begin = frame_begin;
+    p->loaded_end = frame_end;
+    p->prepare_ms = now_ms() - t0;
+    return p;
+}
+
 int gsc_encode_prepared(gsc_prepared* p, int frame_begin, int frame_end, uint8_t** out, size_t* out_len) {
     if (!p || !out || !out_len) return fail("gsc_encode_prepared: null argument");
+    if (p->loaded_end >= 0) {  // a bounds-prepared encoder holds only its own frames' samples
+        const int fe = frame_end < 0 ? p->enc.frame_count() : frame_end;
+        if (frame_begin < p->loaded_begin || fe > p->loaded_end)
+            return fail("gsc_encode_prepared: frames outside the range gsc_prepare_frames loaded");
+    }
     t_tim = gsc_timing{};
     if (encode_prepared(p->enc, frame_begin, frame_end, out, out_len) != 0) return -1;
     t_tim.host_prepare_ms = 0;  // paid once, in gsc_prepare
@@ -1394,6 +1449,44 @@ int gsc_encode_prepared(gsc_prepared* p, int frame_begin, int frame_end, uint8_t
 }
 
 double gsc_prepared_prepare_ms(const gsc_prepared* p) { return p ? p->prepare_ms : 0.0; }
+
+gsc_prepared* gsc_prepare_many(const uint8_t* const* wavs, const size_t* lens, int nfiles, const gsc_options* o) {
+    if (!wavs || !lens || !o || nfiles <= 0) {
+        fail("gsc_prepare_many: invalid argument");
+        return nullptr;
+    }
+    const double t0 = now_ms();
+    gsc_prepared* p = new (std::nothrow) gsc_prepared(*o);
+    if (!p) {
+        fail("gsc_prepare_many: out of host memory");
+        return nullptr;
+    }
+    std::string err;
+    if (p->enc.prepare_many(wavs, lens, nfiles, &err) != 0) {
+        delete p;
+        fail(err);
+        return nullptr;
+    }
+    p->prepare_ms = now_ms() - t0;
+    return p;
+}
+
+int gsc_prepared_file_count(const gsc_prepared* p) { return p ? int(p->enc.file_first().size()) - 1 : -1; }
+
+int gsc_prepared_file_frames(const gsc_prepared* p, int* first_frame) {
+    if (!p || !first_frame) return fail("gsc_prepared_file_frames: null argument");
+    const auto& ff = p->enc.file_first();
+    std::copy(ff.begin(), ff.end(), first_frame);
+    return 0;
+}
+
+int gsc_encode_prepared_files(gsc_prepared* p, int frame_begin, int frame_end, uint8_t** out, size_t* out_len,
+                              size_t* file_bytes) {
+    if (!p || !out || !out_len || !file_bytes) return fail("gsc_encode_prepared_files: null argument");
+    t_tim = gsc_timing{};
+    if (encode_prepared(p->enc, frame_begin, frame_end, out, out_len, file_bytes) != 0) return -1;
+    return 0;
+}
 
 void gsc_prepared_free(gsc_prepared* p) { delete p; }
 

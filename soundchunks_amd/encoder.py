@@ -91,6 +91,17 @@ class Encoder:
         """Load + PrepareFrames once (the frame boundaries of the whole file)."""
         return Prepared(self, wav)
 
+    def prepare_frames(self, wav: bytes, starts, ends, frame_begin: int = 0, frame_end: int = -1) -> "Prepared":
+        """A prepared encoder over frame boundaries computed elsewhere (e.g.
+        broadcast from the rank that ran PrepareFrames); only the samples of
+        frames [frame_begin, frame_end) are loaded and only they may be encoded."""
+        return Prepared(self, wav, bounds=(starts, ends, frame_begin, frame_end))
+
+    def prepare_many(self, wavs) -> "Prepared":
+        """A batch of WAVs as one frame list (each file's own Load +
+        PrepareFrames; every stage then runs one launch for the whole batch)."""
+        return Prepared(self, None, many=list(wavs))
+
     @staticmethod
     def last_timing() -> dict:
         t = _lib.GscTiming()
@@ -103,10 +114,27 @@ class Prepared:
     1294-1429): frame boundaries computed once per job, then any frame range
     encodes without rescanning the file (multi-GPU sharding)."""
 
-    def __init__(self, encoder: Encoder, wav: bytes):
+    def __init__(self, encoder: Encoder, wav: bytes | None, bounds=None, many=None):
         lib = _lib.load()
+        if many is not None:
+            arrs = [_u8(w) for w in many]
+            ptrs = (ctypes.POINTER(ctypes.c_uint8) * len(arrs))(*[p for _, p in arrs])
+            lens = (ctypes.c_size_t * len(arrs))(*[len(a) for a, _ in arrs])
+            h = lib.gsc_prepare_many(ptrs, lens, len(arrs), ctypes.byref(encoder.options))
+            if not h:
+                raise _lib.GscError(lib.gsc_last_error().decode(errors="replace"))
+            self._h = h
+            self.frame_count = lib.gsc_prepared_frame_count(h)
+            self.prepare_ms = lib.gsc_prepared_prepare_ms(h)
+            return
         arr, ptr = _u8(wav)
-        h = lib.gsc_prepare(ptr, len(arr), ctypes.byref(encoder.options))
+        if bounds is None:
+            h = lib.gsc_prepare(ptr, len(arr), ctypes.byref(encoder.options))
+        else:
+            st = np.ascontiguousarray(bounds[0], dtype=np.int32)
+            en = np.ascontiguousarray(bounds[1], dtype=np.int32)
+            h = lib.gsc_prepare_frames(ptr, len(arr), ctypes.byref(encoder.options), _ip(st), _ip(en), len(st),
+                                       int(bounds[2]), int(bounds[3]))
         if not h:
             raise _lib.GscError(lib.gsc_last_error().decode(errors="replace"))
         self._h = h
@@ -119,6 +147,13 @@ class Prepared:
         _lib.check(_lib.load().gsc_prepared_frame_chunks(self._h, _ip(out)))
         return out[: self.frame_count]
 
+    def frame_bounds(self) -> tuple[np.ndarray, np.ndarray]:
+        """First and last sample of every frame (PrepareFrames' cut)."""
+        st = np.zeros(max(1, self.frame_count), dtype=np.int32)
+        en = np.zeros(max(1, self.frame_count), dtype=np.int32)
+        _lib.check(_lib.load().gsc_prepared_frame_bounds(self._h, _ip(st), _ip(en)))
+        return st[: self.frame_count], en[: self.frame_count]
+
     def encode(self, frame_begin: int = 0, frame_end: int = -1) -> bytes:
         lib = _lib.load()
         out = ctypes.POINTER(ctypes.c_uint8)()
@@ -126,6 +161,28 @@ class Prepared:
         _lib.check(lib.gsc_encode_prepared(self._h, frame_begin, frame_end, ctypes.byref(out), ctypes.byref(n)))
         try:
             return ctypes.string_at(out, n.value)
+        finally:
+            lib.gsc_free(out)
+
+    def file_frames(self) -> np.ndarray:
+        """First frame of every file of a batch, then the total frame count."""
+        lib = _lib.load()
+        n = lib.gsc_prepared_file_count(self._h)
+        out = np.zeros(n + 1, dtype=np.int32)
+        _lib.check(lib.gsc_prepared_file_frames(self._h, _ip(out)))
+        return out
+
+    def encode_files(self, frame_begin: int = 0, frame_end: int = -1) -> tuple[bytes, list[int]]:
+        """Frames [frame_begin, frame_end) of the batch: (bytes, per-file byte counts)."""
+        lib = _lib.load()
+        n = lib.gsc_prepared_file_count(self._h)
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        ln = ctypes.c_size_t(0)
+        fb = (ctypes.c_size_t * max(1, n))()
+        _lib.check(lib.gsc_encode_prepared_files(self._h, frame_begin, frame_end, ctypes.byref(out), ctypes.byref(ln),
+                                                 fb))
+        try:
+            return ctypes.string_at(out, ln.value), [int(fb[i]) for i in range(n)]
         finally:
             lib.gsc_free(out)
 
@@ -139,6 +196,29 @@ class Prepared:
             self.close()
         except Exception:
             pass
+
+
+def encode_many(wavs, argv: Sequence[str] = (), rank: int = 0, world_size: int = 1, device=None):
+    """Encode a batch of WAVs (the C4 corpus case) as one job: every frame of
+    every file in one launch per stage, the batch's frame list sharded across
+    ranks by chunk count.  Returns one .gsc per file on rank 0
+    (None on the others; world_size > 1 needs torch.distributed initialised)."""
+    from .shard import frame_range_weighted, gather_files
+
+    wavs = list(wavs)
+    p = Encoder(argv).prepare_many(wavs)
+    try:
+        b, e = frame_range_weighted(p.frame_chunks().tolist(), rank, world_size)
+        blob, sizes = p.encode_files(b, e)
+    finally:
+        p.close()
+    if world_size > 1:
+        return gather_files(blob, sizes, device=device)
+    outs, o = [], 0
+    for n in sizes:
+        outs.append(blob[o:o + n])
+        o += n
+    return outs
 
 
 def set_device(device: int) -> None:

@@ -23,23 +23,28 @@ def wav_header(channels: int, rate: int, n_frames: int) -> bytes:
     )
 
 
-def synth_pcm(seconds: float, rate: int = 44100, channels: int = 2, seed: int = SEED) -> np.ndarray:
-    """Interleaved int16 samples, shape (n_frames, channels)."""
+def synth_pcm(seconds: float, rate: int = 44100, channels: int = 2, seed: int = SEED,
+              chunk: int = 1 << 22) -> np.ndarray:
+    """Interleaved int16 samples, shape (n_frames, channels).  Generated in
+    chunks (the normal stream of one Generator is the same whether drawn at
+    once or in pieces), so a long signal never holds n float64 temporaries."""
     n = int(round(seconds * rate))
     rng = np.random.Generator(np.random.PCG64(seed))
-    t = np.arange(n, dtype=np.float64) / rate
     freqs = [440.0, 660.0]
     out = np.empty((n, channels), dtype=np.int16)
-    for c in range(channels):
-        x = 0.25 * np.sin(2.0 * np.pi * freqs[c % 2] * t) + 0.05 * rng.standard_normal(n)
-        x = np.clip(x, -1.0, 1.0)
-        out[:, c] = np.round(x * 32767.0).astype(np.int16)
+    for c in range(channels):  # channel 0's noise first, then channel 1's
+        for a in range(0, n, chunk):
+            b = min(n, a + chunk)
+            t = np.arange(a, b, dtype=np.float64) / rate
+            x = 0.25 * np.sin(2.0 * np.pi * freqs[c % 2] * t) + 0.05 * rng.standard_normal(b - a)
+            x = np.clip(x, -1.0, 1.0)
+            out[a:b, c] = np.round(x * 32767.0).astype(np.int16)
     return out
 
 
 def synth_wav(seconds: float, rate: int = 44100, channels: int = 2, seed: int = SEED) -> bytes:
     pcm = synth_pcm(seconds, rate, channels, seed)
-    return wav_header(channels, rate, pcm.shape[0]) + pcm.astype("<i2").tobytes()
+    return wav_header(channels, rate, pcm.shape[0]) + pcm.astype("<i2", copy=False).tobytes()
 
 
 if __name__ == "__main__":  # pragma: no cover

@@ -74,6 +74,9 @@ def load():
         lib.ora_get_stats.argtypes = [ctypes.POINTER(OraStats)]
         lib.ora_trace_frame.argtypes = [u8p, ctypes.c_size_t, ctypes.POINTER(OraParams), ctypes.c_int,
                                         ctypes.POINTER(OraTrace)]
+        lib.ora_frame_bounds.argtypes = [u8p, ctypes.c_size_t, ctypes.POINTER(OraParams), ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_int]
+        lib.ora_frame_bounds.restype = ctypes.c_int
         lib.ora_decode.argtypes = [u8p, ctypes.c_size_t, ctypes.POINTER(ctypes.POINTER(ctypes.c_int16)),
                                    ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         lib.ora_decode.restype = ctypes.c_long
@@ -209,6 +212,21 @@ def decode(gsc: bytes):
     out = np.ctypeslib.as_array(pcm, shape=(n,)).copy() if n > 0 else np.zeros(0, np.int16)
     lib.ora_free(pcm)
     return out, ch.value, rate.value
+
+
+def frame_bounds(wav: bytes, argv=()):
+    """PrepareFrames' frame boundaries: (starts, ends) int32 arrays."""
+    lib = load()
+    p = params(argv)
+    a, ptr = _u8(wav)
+    n = lib.ora_frame_bounds(ptr, len(a), ctypes.byref(p), None, None, 0)
+    if n < 0:
+        raise RuntimeError(f"oracle prepare failed: {n}")
+    st = np.zeros(max(n, 1), np.int32)
+    en = np.zeros(max(n, 1), np.int32)
+    lib.ora_frame_bounds(ptr, len(a), ctypes.byref(p), st.ctypes.data_as(ctypes.c_void_p),
+                         en.ctypes.data_as(ctypes.c_void_p), n)
+    return st[:n], en[:n]
 
 
 def trace_frame(wav: bytes, argv=(), frame: int = 0) -> dict:

@@ -177,6 +177,27 @@ def test_corpus_matches_oracle(name):
     assert hashlib.sha256(got).hexdigest() == want["gsc_sha256"]
 
 
+def test_corpus_as_one_batch_matches_oracle():
+    """C4 (BASELINE configs[3]): all 22 corpus files in ONE batched encode --
+    every frame of every file in one launch per stage (gsc_prepare_many /
+    gsc_encode_prepared_files) -- and each file's .gsc equals the oracle's."""
+    import hashlib
+
+    import soundchunks_amd as sc
+    from golden.cases import HERE
+
+    meta = _corpus()
+    names = sorted(meta["files"])
+    wavs = [(HERE / "lame_test" / n).read_bytes() for n in names]
+    outs = sc.encode_many(wavs, meta["argv"])
+    tm = sc.Encoder.last_timing()
+    assert tm["frames"] == sum(meta["files"][n]["frames"] for n in names)
+    assert tm["scan_launches"] < len(names)  # batched launch rounds, not one per file
+    for n, got in zip(names, outs):
+        assert len(got) == meta["files"][n]["gsc_bytes"], n
+        assert hashlib.sha256(got).hexdigest() == meta["files"][n]["gsc_sha256"], n
+
+
 # f4: reconstruction (TBand/TEncoder.MakeDstData) and PsyADelta on the device
 @pytest.mark.parametrize("name", ["c1_test_cs8_cpf256", "hihat_cs4_default", "syn3s_cs8_cpf1000_cbd12",
                                   "syn8s_c3_cs16_cpf4096_cbd12", "tiny_passthrough_cs8", "quiet_tone_cs8_cpf1024"])

@@ -1,0 +1,93 @@
+"""The multi-GPU plumbing bench.py uses (soundchunks_amd.shard), on CPU:
+the --gpus N launcher, rank 0's PrepareFrames boundaries broadcast to every
+rank, the chunk-count (LPT) frame ranges, a rank preparing only its own
+frames from the broadcast bounds, and the frame-ordered / per-file gathers.
+World size 2 over gloo; the per-rank encoder is the oracle (the CPU checker:
+the HIP encoder needs the GPU, tests/test_shard.py runs it there)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def test_spawn_workers_sets_rank_env(tmp_path):
+    from soundchunks_amd.shard import spawn_workers
+
+    script = tmp_path / "w.py"
+    out = tmp_path / "out"
+    out.mkdir()
+    script.write_text("import os, pathlib\n"
+                      f"pathlib.Path(r'{out}', os.environ['RANK']).write_text("
+                      "os.environ['WORLD_SIZE'] + ' ' + os.environ['LOCAL_RANK'] + ' ' + os.environ['MASTER_ADDR'])\n")
+    assert spawn_workers(3, [sys.executable, str(script)]) == 0
+    got = sorted((p.name, p.read_text()) for p in out.iterdir())
+    assert got == [("0", "3 0 127.0.0.1"), ("1", "3 1 127.0.0.1"), ("2", "3 2 127.0.0.1")]
+    bad = tmp_path / "bad.py"
+    bad.write_text("import os, sys, time\nif os.environ['RANK'] == '1': sys.exit(7)\ntime.sleep(30)\n")
+    assert spawn_workers(2, [sys.executable, str(bad)]) == 7  # rank 1 fails: rank 0 is ended, not waited for
+
+
+def test_bench_refuses_mismatched_world_size():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "3", "--no-cpu-baseline"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+
+
+def _job_worker(rank, ws, port, argv, q):
+    sys.path[:0] = [str(ROOT), str(ROOT / "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    import oracle_ffi
+    import soundchunks_amd as sc
+    from golden.cases import _tone_lsb
+    from soundchunks_amd.shard import bounds_range, broadcast_bounds, gather_files, gather_streams
+
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        wav = _tone_lsb(6.0)
+        enc = sc.Encoder(argv)
+        st = en = None
+        if rank == 0:  # PrepareFrames of the whole file (the product's host code) on rank 0 only
+            st, en = enc.prepare(wav).frame_bounds()
+        st, en = broadcast_bounds(st, en)
+        b, e = bounds_range(st, en, enc.chunk_size, 1, rank, ws)
+        mine = enc.prepare_frames(wav, st, en, b, e)  # only this rank's samples
+        assert mine.frame_count == len(st)
+        blob, _ = oracle_ffi.encode_frames(wav, argv, b, e, threads=2)
+        whole = gather_streams(blob)
+        per_file = gather_files(b"r%d" % rank * 3, [2, 4])  # two files: 2 + 4 bytes from each rank
+        if rank == 0:
+            q.put((len(st), (b, e), whole, per_file))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_job_equals_single_encode():
+    import oracle_ffi
+    from golden.cases import _tone_lsb
+
+    argv = ["-cs8", "-cpf256", "-fl1000"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31500 + (os.getpid() % 1000)
+    procs = [ctx.Process(target=_job_worker, args=(r, 2, port, argv, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    nfr, rng0, whole, per_file = q.get(timeout=280)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert nfr >= 4 and 0 < rng0[1] < nfr
+    assert whole == oracle_ffi.encode(_tone_lsb(6.0), argv, threads=4)
+    assert per_file == [b"r0" + b"r1", b"r0r0" + b"r1r1"]

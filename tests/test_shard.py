@@ -82,13 +82,20 @@ def _hip_worker(rank, ws, port, name, q):
 
     import soundchunks_amd as sc
     from golden.cases import CASES
-    from soundchunks_amd.shard import frame_range_weighted, gather_streams
+    from soundchunks_amd.shard import gather_streams
 
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     try:
+        from soundchunks_amd.shard import bounds_range, broadcast_bounds
+
         make, argv = CASES[name]
-        prep = sc.Encoder(argv).prepare(make())  # PrepareFrames once per job
-        b, e = frame_range_weighted(prep.frame_chunks().tolist(), rank, ws)
+        wav = make()
+        enc = sc.Encoder(argv)
+        prep = enc.prepare(wav) if rank == 0 else None  # PrepareFrames once per job, on rank 0
+        st, en = broadcast_bounds(*(prep.frame_bounds() if prep is not None else (None, None)))
+        b, e = bounds_range(st, en, enc.chunk_size, 1, rank, ws)
+        if prep is None:  # the other ranks load only their frames' samples (bench.py's path)
+            prep = enc.prepare_frames(wav, st, en, b, e)
         out = gather_streams(prep.encode(b, e))
         if rank == 0:
             q.put((prep.frame_count, (b, e), out))
