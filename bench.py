@@ -21,7 +21,7 @@ Scaling: weak by default (each rank adds --seconds of audio to one longer
 file); --strong keeps one --seconds file for any world size.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--seconds S]
-                  [--config c1|c2|c3|c4|c5|c5cs4] [--strong] [--no-cpu-baseline]
+                  [--config c1|c2|c3|c4|c5|c5cs4|br128] [--strong] [--no-cpu-baseline]
 
 --gpus N without a launcher's WORLD_SIZE spawns N worker processes (one per
 GPU, RANK/LOCAL_RANK/WORLD_SIZE, rendezvous at 127.0.0.1) before any GPU call.
@@ -47,6 +47,9 @@ CONFIGS = {
     # configs[4]'s signal (48 kHz stereo, ChunkCount=4096) at both ChunkSizes SURVEY.md §8 names
     "c5": (["-cs8", "-cpf4096"], 2, 48000, 8, "48 kHz stereo, ChunkSize=8 ChunkCount=4096"),
     "c5cs4": (["-cs4", "-cpf4096"], 2, 48000, 4, "48 kHz stereo, ChunkSize=4 ChunkCount=4096"),
+    # the reference's own -br invocation (encoder/encoder.lps:270-279): ChunksPerFrame from the
+    # bit-rate cost loop (encoder.lpr:1337-1351), not a power of two (485 at 44.1 kHz stereo)
+    "br128": (["-br128", "-vfr0.5", "-cs8"], 2, 44100, 8, "44.1 kHz stereo, -br128 -vfr0.5 ChunkSize=8"),
     # configs[3]: the reference's lame_test corpus (22 mono 44.1 kHz files) as one batch, default flags
     "c4": (["-cs8", "-cpf4096"], 1, 44100, 8, "lame_test corpus (22 mono 44.1 kHz files), ChunkSize=8 ChunkCount=4096"),
 }

@@ -31,7 +31,7 @@ extern "C" hipError_t gsc_launch_scan_pass(int D, gsc::ReduceFrame* frames, int 
                                            int only_flagged, hipStream_t st);
 extern "C" hipError_t gsc_launch_scan_batch(int D, int logk, gsc::ReduceFrame* frames, int nframes, const float* X,
                                             float* C, int* is, const float* rate_tab, double tol, int max_passes,
-                                            uint64_t* xbuf, hipStream_t st);
+                                            uint64_t* xbuf, int opts, hipStream_t st);
 extern "C" size_t gsc_scan_xbuf_granules_per_frame(void);
 extern "C" hipError_t gsc_launch_atten(int cs, gsc::DspFrame* frames, int nframes, const double* samp, int64_t span,
                                        int ch, int obd, hipStream_t st);
@@ -176,11 +176,21 @@ double scan_tolerance(int precision) {
     return 1.0 / p;
 }
 
-// K = 2^logk in [256, 4096] and D in {8, 16, 32}: the batched speculative
-// kernel (gsc_scan.hip) covers the pass; anything else runs the generic kernel.
+// leaves of the batched kernel's layout: K rounded up to a power of two, at
+// least 256 (a K below it runs the padded layout, gsc_tree.h pad_tree)
+int padded_k(int K) {
+    int k = 256;
+    while (k < K) k <<= 1;
+    return k;
+}
+
+// D in {8, 16, 32} and 2 <= K <= 4096: the batched speculative kernel
+// (gsc_scan.hip) covers the pass (K = 4096 at D = 32 on two CUs per frame,
+// which has no padded form: D = 32 with 2048 < K < 4096 runs the generic kernel).
 bool batched_scan_shape(int D, int K) {
     if (std::getenv("GSC_SCAN_GENERIC")) return false;  // diagnostic switch
-    return (D == 8 || D == 16 || D == 32) && K >= 256 && K <= 4096 && (K & (K - 1)) == 0;
+    if (!(D == 8 || D == 16 || D == 32) || K < 2 || K > 4096) return false;
+    return !(D == 32 && K > 2048 && K != 4096);
 }
 
 // D = 32 at K = 4096 runs each frame on two CUs, which hand data over through
@@ -206,7 +216,7 @@ hipError_t launch_scan_passes(int D, ReduceFrame* dfr, int nf, int K, const floa
         if (e != hipSuccess) return e;
     }
     int logk = 0;
-    while ((1 << logk) < K) ++logk;
+    while ((1 << logk) < padded_k(K)) ++logk;
     int max_passes = kMaxScanIters;
     if (const char* e = std::getenv("GSC_SCAN_MAX_PASSES")) max_passes = std::max(1, std::min(kMaxScanIters, std::atoi(e)));
     // every launch advances each live frame by at least one pass (the batched
@@ -215,7 +225,10 @@ hipError_t launch_scan_passes(int D, ReduceFrame* dfr, int nf, int K, const floa
     std::vector<int32_t> done(static_cast<size_t>(nf));
     for (int round = 0; round < max_passes; ++round) {
         if (batched) {
-            const hipError_t e = gsc_launch_scan_batch(D, logk, dfr, nf, X, C, is, rate, tol, max_passes, xbuf.p, nullptr);
+            // opts bit 0 (diagnostic GSC_SCAN_FULL_A1): full-dimension A1 bounds in every pass
+            const int opts = std::getenv("GSC_SCAN_FULL_A1") ? 1 : 0;
+            const hipError_t e =
+                gsc_launch_scan_batch(D, logk, dfr, nf, X, C, is, rate, tol, max_passes, xbuf.p, opts, nullptr);
             if (e != hipSuccess) return e;
         }
         const hipError_t e = gsc_launch_scan_pass(D, dfr, nf, K, X, C, is, fs, rate, tol, max_passes, batched ? 1 : 0, nullptr);
@@ -270,9 +283,10 @@ int run_reduce_batch_dev(int D, int K, int precision, const std::vector<int>& Ns
         no += Ns[i];
         maxN = std::max<int64_t>(maxN, Ns[i]);
     }
+    const int Kp = padded_k(K);  // per-position scratch covers the padded layout
     for (int i = 0; i < nf; ++i) {
         fr[i].k_off = no + int64_t(i) * K;
-        fr[i].ka_off = no + int64_t(nf + i) * K;
+        fr[i].ka_off = no + int64_t(nf) * K + int64_t(i) * Kp;
         if (cl_host && notify) {
             fr[i].cl_host = cl_host + fr[i].n_off;
             fr[i].notify = notify + i;
@@ -284,7 +298,7 @@ int run_reduce_batch_dev(int D, int K, int precision, const std::vector<int>& Ns
     DevBuf<ReduceFrame> dFr;
     HIP_TRY(dC.alloc(size_t(nf) * K * D));
     HIP_TRY(dF.alloc(size_t(no) * 4));
-    HIP_TRY(dI.alloc(size_t(no) + 2 * size_t(nf) * K));
+    HIP_TRY(dI.alloc(size_t(no) + size_t(nf) * (size_t(K) + size_t(Kp))));
     HIP_TRY(dBits.alloc(size_t(no / 32) + size_t(nf) * 2 + 2));
     HIP_TRY(dFr.alloc(size_t(nf)));
     const std::vector<float> rt = rate_table(int(maxN));
@@ -1614,7 +1628,7 @@ int gsc_scan_reduce(int n, int d, const float* x, int k, float* centroids, int* 
     HIP_TRY(dF.alloc(size_t(n) * 4));
     HIP_TRY(dX.alloc(size_t(n) * d));
     HIP_TRY(dC.alloc(size_t(k) * d));
-    HIP_TRY(dI.alloc(size_t(n) + 2 * size_t(k)));
+    HIP_TRY(dI.alloc(size_t(n) + size_t(k) + size_t(padded_k(k))));
     HIP_TRY(dFr.alloc(1));
     const std::vector<float> rt = rate_table(n);
     HIP_TRY(dRate.alloc(rt.size()));

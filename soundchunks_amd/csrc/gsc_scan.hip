@@ -74,6 +74,7 @@ struct ScanCfg {
     static constexpr int KB = D > 16 ? 16 : 32;                         // queries per speculative batch
     static constexpr int KVER = 64 + KB;                                // centroid versions a pending batch sees
     static constexpr int QD = D < 16 ? 16 : D;                          // query row stride
+    static constexpr int H = D / 2;  // DCT half of the features; [H, D) = cepstrum x 1e-5 (encoder.lpr:1700-1716)
     static constexpr int ROW = D + 4;  // lane-indexed coordinate rows: 16-B multiple, odd x 16 B (no b128 conflicts)
     // A1 bound slack: eps(q) = (|q|^2 + M) * 2^-EPSX (see a1_dist_x2)
     static constexpr float EPSF = D > 16 ? 0x1p-16f : 0x1p-17f;
@@ -162,6 +163,11 @@ struct Scan2Shared {
     alignas(16) float q[2][C::KB][C::QD];
     alignas(16) float qm[2][C::KB][C::QD];  // -2 q (exact), the A1 dot-product operand
     float cnmax[C::NWV];   // per (virtual) wave: upper bound of |c|^2 over its live centroids (monotone within a pass)
+    // half-dimension A1 (see a1_dist_x2): per-wave |c_h|^2 / |c|^2 maxima and
+    // tail-dimension boxes at pass start, the frame's data tail box (order keys)
+    float cnmax_h[C::NWV], cnmax_f[C::NWV];
+    float ptlo[C::NWV][C::D], pthi[C::NWV][C::D];
+    int xtlo[C::D], xthi[C::D];
     // A1 pruning (one-CU frames): per wave the bounding box of its centroids'
     // live register coordinates (grown by every fold), per batch query an
     // upper bound of the snapshot's minimum distance
@@ -177,6 +183,7 @@ struct Scan2Shared {
     alignas(16) float solo_c[C::ROW];  // coordinates of the solo query's centroid
     double err_out;
     // commit of the pending batch: versions 0..63 = log entries, 64+j = after query j
+    int vcs[C::KB];        // c* of the pending batch's queries (-2 past the batch)
     int vpos[C::KVER];
     int vfrom[C::KVER];    // first query that sees the version
     int vto[C::KVER];      // last query that sees it
@@ -370,13 +377,13 @@ __device__ __forceinline__ int wave_max_i(int v) {
 // pass start: the box of this wave's leaves
 template <class C>
 __device__ __forceinline__ void wave_box_init(Scan2Shared<C>& sh, const float (&creg)[C::SL][C::D], int vwave, int lane,
-                                              int p0) {
+                                              int p0, uint32_t dmask) {
 #pragma unroll  // static register indices: a runtime d would demote creg to scratch
     for (int d = 0; d < C::D; ++d) {
         float lo = __builtin_inff(), hi = -__builtin_inff();
 #pragma unroll
         for (int s = 0; s < C::SL; ++s)
-            if (p0 + s < C::K) {
+            if (!((dmask >> s) & 1u)) {
                 lo = fminf(lo, creg[s][d]);
                 hi = fmaxf(hi, creg[s][d]);
             }
@@ -500,9 +507,11 @@ __device__ __forceinline__ void a1_reduce2(const float (&dv0)[C::SL], const floa
 
 template <class C>
 __device__ __forceinline__ void a1_query(const float (&creg)[C::SL][C::D], const float* __restrict__ qv,
-                                         WaveRecT<C::SL>& rec, int vwave, int lane) {
+                                         WaveRecT<C::SL>& rec, int vwave, int lane, uint32_t dmask) {
     float dv[C::SL];
     a1_dist<C::D, C::SL>(creg, qv, dv);
+#pragma unroll
+    for (int s = 0; s < C::SL; ++s) dv[s] = ((dmask >> s) & 1u) ? __builtin_inff() : dv[s];  // padding leaves
     a1_reduce<C>(dv, rec, vwave, lane);
 }
 
@@ -521,7 +530,19 @@ __device__ __forceinline__ void a1_query(const float (&creg)[C::SL][C::D], const
 // snapshot (fixup in part 2).  The committed distance g is always recomputed
 // exactly from c*'s coordinates (vp_end).
 // ---------------------------------------------------------------------------
-template <int D, int SL>
+//
+// Half-dimension bounds (per pass, one-CU frames): the features [H, D) are the
+// cepstrum scaled by 1e-5 (encoder.lpr:1700-1716), so their share of any
+// distance is at most TW = sum_{d >= H} (hi_d - lo_d)^2 over the box of the
+// frame's data and the pass's centroids (every centroid stays in that box: a
+// move is c + (x - c) * rate with rate <= 1, widened by an ulp slack).  With
+// DD = H the bound covers the first H features only; the certificate then uses
+// |q_h|^2 + TW/2 for |q|^2 and eps + TE for eps, TE = TW/2 + EPSF * (tail
+// norms), which keeps every inequality of A2 and of the pruning sound.  A pass
+// uses it only when TE is small against the norm scale of eps (else the full
+// D-dimension bound, as before).
+// ---------------------------------------------------------------------------
+template <int DD, int D, int SL>
 __device__ __forceinline__ void a1_dist_x2(const float (&creg)[SL][D], const float (&cn)[SL],
                                            const float* __restrict__ qm0, const float* __restrict__ qm1,
                                            float (&dv0)[SL], float (&dv1)[SL]) {
@@ -531,7 +552,7 @@ __device__ __forceinline__ void a1_dist_x2(const float (&creg)[SL][D], const flo
         dv1[s] = cn[s];
     }
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
+    for (int d = 0; d < DD; ++d) {
         const float m0 = qm0[d], m1 = qm1[d];
 #pragma unroll
         for (int s = 0; s < SL; ++s) {
@@ -573,7 +594,8 @@ __device__ __forceinline__ float fsum16(float v) {  // sum over each aligned 16-
 // ---------------------------------------------------------------------------
 template <class C, bool APPROX>
 __device__ __forceinline__ void a2_group(Scan2Shared<C>& sh, int j0, int nq, const float (*qrows)[C::QD],
-                                         QRecT<C::D>* recs, int wcol0, const int* jlist, int lane
+                                         QRecT<C::D>* recs, int wcol0, const int* jlist, int lane,
+                                         bool half = false, float twh = 0.0f, float te = 0.0f
 #ifdef GSC_STAMPS
                                          , uint64_t* acc = nullptr, uint64_t* tl = nullptr
 #endif
@@ -696,13 +718,15 @@ __device__ __forceinline__ void a2_group(Scan2Shared<C>& sh, int j0, int nq, con
     float m2lo;
     if constexpr (APPROX) {
         // A1 values are within eps of the reference's distances: certify with margins
-        const float qs = l < D ? q[l] : 0.0f;
-        const float qs2 = (D > 16 && l + 16 < D) ? q[l + 16] : 0.0f;
-        const float qn = fsum16(__builtin_fmaf(qs2, qs2, __builtin_fmaf(qs, qs, 0.0f)));
+        const int dn = half ? C::H : D;  // features the A1 bounds cover
+        const float qs = l < dn ? q[l] : 0.0f;
+        const float qs2 = (D > 16 && l + 16 < dn) ? q[l + 16] : 0.0f;
+        const float qn0 = fsum16(__builtin_fmaf(qs2, qs2, __builtin_fmaf(qs, qs, 0.0f)));
         float M = 0.0f;
 #pragma unroll
         for (int w = 0; w < NW; ++w) M = fmaxf(M, sh.cnmax[w]);
-        const float eps = fadd(fmul(fadd(qn, M), C::EPSF), 1e-37f);
+        const float eps = fadd(fadd(fmul(fadd(qn0, M), C::EPSF), 1e-37f), te);
+        const float qn = fadd(qn0, twh);  // the tail's midpoint (0 in full-dimension passes)
         ok = !far || (fsub(fadd(qn, __uint_as_float(sib)), eps) > Bv);
         unique = fsub(__uint_as_float(m2), __uint_as_float(gmin)) > fadd(eps, eps);
         m2lo = fsub(fadd(qn, __uint_as_float(m2)), eps);
@@ -738,8 +762,7 @@ __device__ __forceinline__ void a2_group(Scan2Shared<C>& sh, int j0, int nq, con
 // assuming every query of the batch commits; version table for the checks.
 // Log entry e is lane e: position lg_pos (-1 = empty), tag = commit iteration.
 // ---------------------------------------------------------------------------
-// Scan state of one pending query (lane j) / log entry (lane e), built one
-// step per A1 query so the LDS round trips hide under wave 0's distance work.
+// Scan state of one pending query (lane j) / log entry (lane e).
 struct VPState {
     int cs, pred, nxt, first, ie;
 };
@@ -749,26 +772,32 @@ __device__ __forceinline__ void vp_begin(Scan2Shared<C>& sh, int qb, int off, in
                                          int lg_tag, VPState& st) {
     if (lg_pos >= 0 && lg_tag < a1) lg_pos = -1;  // committed before the batch's snapshot
     st.cs = lane < pn ? sh.qrec[qb][off + lane].cstar : -2;
-    st.pred = -1;
-    st.nxt = C::KB;
-    st.first = C::KB;
-    st.ie = 64;
     sh.vpos[lane] = lg_pos;
     sh.vfrom[lane] = 0;
+    if (lane < C::KB) sh.vcs[lane] = st.cs;
     wave_lds_sync();
-}
-
-// step k (uniform): pending query k against every lane's query / entry, all
-// in registers (c*_k by readlane, the entries holding it by ballot)
-template <class C>
-__device__ __forceinline__ void vp_step(int k, int lane, int lg_pos, VPState& st) {
-    const int ck = __builtin_amdgcn_readlane(st.cs, k);  // -2 past the batch: matches nothing
-    const bool same = ck == st.cs;
-    if (k < lane && same) st.pred = 64 + k;
-    if (k > lane && same && st.nxt == C::KB) st.nxt = k;
-    if (ck == lg_pos && st.first == C::KB) st.first = k;  // lane as log entry: first query moving it
-    const uint64_t em = __ballot(lg_pos == ck);            // entries holding c*_k (lowest = ie_k)
-    if (lane == k && em) st.ie = __ffsll((long long)em) - 1;
+    // every lane against every pending query / log entry at once: the c* of
+    // the KB queries and the 64 entries' positions are LDS broadcasts, so no
+    // step waits for the previous one (the serial readlane / ballot chain
+    // this replaces kept wave 0 ~7k cycles behind the others at the A1 barrier)
+    const int cs = st.cs;
+    int pred = -1, nxt = C::KB, first = C::KB, ie = 64;
+#pragma unroll
+    for (int k = 0; k < C::KB; ++k) {
+        const int ck = sh.vcs[k];  // -2 past the batch: matches no entry
+        const bool same = ck == cs;
+        pred = (k < lane && same) ? 64 + k : pred;               // last earlier query with the same c*
+        nxt = (k > lane && same && nxt == C::KB) ? k : nxt;      // first later one
+        first = (ck == lg_pos && first == C::KB) ? k : first;    // lane as log entry: first query moving it
+    }
+    if (lane < C::KB) {
+#pragma unroll
+        for (int e = 63; e >= 0; --e) ie = sh.vpos[e] == cs ? e : ie;  // lowest entry holding c*_j
+    }
+    st.pred = pred;
+    st.nxt = nxt;
+    st.first = first;
+    st.ie = ie;
 }
 
 template <class C>
@@ -1145,10 +1174,11 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                                                            const float* __restrict__ Xall, float* __restrict__ Call,
                                                            int* __restrict__ i_scratch,
                                                            const float* __restrict__ rate_tab, double tol,
-                                                           int max_passes, uint64_t* __restrict__ xbuf) {
+                                                           int max_passes, uint64_t* __restrict__ xbuf, int opts) {
     constexpr int D = C::D, K = C::K, SL = C::SL, LS = C::LS, NWL = C::NWL, KB = C::KB, NWG = C::NWG;
     constexpr int kErrWave = NWL > 1 ? 1 : 0;  // residual + cluster ids (wave 0 keeps the log)
     constexpr bool PRUNE = NWG == 1;           // A1 pruning by wave boxes (one-CU frames)
+    const bool no_half = (opts & 1) != 0;      // diagnostic: full-dimension A1 bounds in every pass
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Scan2Shared<C>& sh = *reinterpret_cast<Scan2Shared<C>*>(smem);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1171,6 +1201,11 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     ReduceFrame* frp = frames + fi;
     if (uniform_int(frp->done) || uniform_int(frp->generic)) continue;
     const int N = uniform_int(frp->N);
+    // ChunksPerFrame that is not a power of two (the -br cost loop,
+    // encoder.lpr:1337-1351): ANN's tree over the Kr centroids, embedded in the
+    // K = 2^LOGK leaf layout with padding leaves that are never visited (pad_tree)
+    const int Kr = NWG == 1 ? uniform_int(frp->K) : K;
+    const bool padded = Kr != K;
     const float* __restrict__ X = uniform_ptr(Xall + frp->x_off);
     float* C_ = uniform_ptr(Call + frp->c_off);
     int* clusters = uniform_ptr(i_scratch + frp->n_off);
@@ -1183,6 +1218,26 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         xp.seq = (uint32_t)uniform_int(frp->xseq);
     }
     double prev_err = uniform_int(frp->iters) == 0 ? 3.4028234663852886e+38 : frp->err;  // err := MaxSingle
+    if constexpr (PRUNE) {  // box of the frame's data in the tail features (half-dimension A1 bounds)
+        constexpr int NT_ = D - C::H;
+        static_assert(nthreads % NT_ == 0, "each thread keeps one tail feature");
+        __syncthreads();  // the previous frame's readers are done
+        if (tid < D) {
+            sh.xtlo[tid] = 0x7FFFFFFF;
+            sh.xthi[tid] = (int)0x80000000;
+        }
+        __syncthreads();
+        int klo = 0x7FFFFFFF, khi = (int)0x80000000;
+        const int d = C::H + tid % NT_;
+        for (int64_t r = tid / NT_; r < N; r += nthreads / NT_) {
+            const int k = ordkey(__float_as_uint(X[r * D + d]));
+            klo = min(klo, k);
+            khi = max(khi, k);
+        }
+        atomicMin(&sh.xtlo[d], klo);
+        atomicMax(&sh.xthi[d], khi);
+        __syncthreads();
+    }
 
     // All of the frame's passes run in this launch (the pass index lives in
     // the frame descriptor), so a frame never waits for the slowest frame of a
@@ -1192,40 +1247,69 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     const uint64_t t_kernel0 = stamp();
 #endif
     if (pass == 0 && wg0)
-        for (int k = tid; k < K; k += nthreads) prev_cnt[k] = 1;  // CCntStart (encoder.lpr:717-721)
+        for (int k = tid; k < Kr; k += nthreads) prev_cnt[k] = 1;  // CCntStart (encoder.lpr:717-721)
     if (tid == 0) sh.any_nan = 0;
     if constexpr (NWG == 2) {
         if (pass == 0) pair_barrier(xp, tid);  // workgroup 1 reads prev_cnt below: workgroup 0 wrote it
     }
     __syncthreads();
-    if (!build_tree_fast<D, C::LOGK, nthreads>(sh.t, sh.dist, sh.dfs_inc, C_, &sh.slow_pos)) {
+    if (padded) {
+        build_tree<D>(sh.t, sh.dist, C_, Kr);  // ANN's n/2 splits over the real centroids
+        pad_tree<C::LOGK>(sh.t, reinterpret_cast<int*>(sh.dist), Kr, tid, nthreads);
+    } else if (!build_tree_fast<D, C::LOGK, nthreads>(sh.t, sh.dist, sh.dfs_inc, C_, &sh.slow_pos)) {
         build_tree<D>(sh.t, sh.dist, C_, K);  // median ties: quickselect's exact order
         if (tid == 0 && wg0) frp->tree_exact += 1;
     }
 
     float creg[SL][D];
-    float cn[SL];  // |c|^2 per register leaf (A1 bounds)
+    float cn[SL];  // |c|^2 per register leaf (A1 bounds); +inf for padding leaves
     const int p0 = (vwave * 64 + lane) * SL;
     bool nan_here = false;
+    uint32_t dmask = 0;  // slots that hold no centroid (past K, or padding leaves)
 #pragma unroll
     for (int s = 0; s < SL; ++s) {
         const int p = p0 + s;
-        if (p < K) {
-            const int id = sh.t.pidx[p];
+        const int id = p < K ? (int)sh.t.pidx[p] : 0xFFFF;
+        if (id != 0xFFFF) {
 #pragma unroll
             for (int d = 0; d < D; ++d) {
                 creg[s][d] = C_[(int64_t)id * D + d];
                 nan_here |= creg[s][d] != creg[s][d];
             }
         } else {
+            dmask |= 1u << s;
 #pragma unroll
             for (int d = 0; d < D; ++d) creg[s][d] = 0.0f;
         }
-        cn[s] = norm2_x<D>(creg[s]);
+        cn[s] = id != 0xFFFF ? norm2_x<D>(creg[s]) : __builtin_inff();
+    }
+    if constexpr (PRUNE) {  // the half-dimension bound's inputs: H-norm maxima, tail box of the centroids
+        float mh = 0.0f;
+#pragma unroll
+        for (int s = 0; s < SL; ++s) mh = fmaxf(mh, (dmask >> s) & 1u ? 0.0f : norm2_x<C::H>(creg[s]));
+        mh = wave_max_nonneg(nan_here ? 0.0f : mh);
+        if (lane == 0) sh.cnmax_h[vwave] = mh;
+#pragma unroll
+        for (int d = C::H; d < D; ++d) {
+            float lo = __builtin_inff(), hi = -__builtin_inff();
+#pragma unroll
+            for (int s = 0; s < SL; ++s)
+                if (!((dmask >> s) & 1u)) {
+                    lo = fminf(lo, creg[s][d]);
+                    hi = fmaxf(hi, creg[s][d]);
+                }
+            const int klo = wave_min_i(ordkey(__float_as_uint(lo)));
+            const int khi = wave_max_i(ordkey(__float_as_uint(hi)));
+            if (lane == 0) {
+                sh.ptlo[vwave][d] = __uint_as_float(keybits(klo));
+                sh.pthi[vwave][d] = __uint_as_float(keybits(khi));
+            }
+        }
     }
     // rates of every position (both workgroups of a two-CU frame commit any c*)
     for (int p = tid; p < K; p += nthreads) {
-        sh.rate[p] = rate_tab[prev_cnt[sh.t.pidx[p]]];  // Single(1/sqrt(cnts[not Odd(iter)]))
+        const int id = sh.t.pidx[p];
+        sh.rate[p] = id != 0xFFFF ? rate_tab[prev_cnt[id]] : 0.0f;  // Single(1/sqrt(cnts[not Odd(iter)]))
         if (wg0) cnta[p] = 1;
     }
     if (nan_here) sh.any_nan = 1;
@@ -1233,12 +1317,15 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     {
         float mx = 0.0f;
 #pragma unroll
-        for (int s = 0; s < SL; ++s) mx = fmaxf(mx, cn[s]);
+        for (int s = 0; s < SL; ++s) mx = fmaxf(mx, (dmask >> s) & 1u ? 0.0f : cn[s]);
         cnmax = wave_max_nonneg(nan_here ? 0.0f : mx);  // NaN passes leave for the generic kernel below
-        if (lane == 0) sh.cnmax[vwave] = cnmax;
+        if (lane == 0) {
+            sh.cnmax[vwave] = cnmax;
+            sh.cnmax_f[vwave] = cnmax;
+        }
     }
     if constexpr (PRUNE) {
-        wave_box_init<C>(sh, creg, vwave, lane, p0);
+        wave_box_init<C>(sh, creg, vwave, lane, p0, dmask);
         if (tid < KB) sh.ub[tid] = kInfBits;
     }
     // first batch's queries
@@ -1259,6 +1346,35 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         if (tid == 0 && sh.xnan) sh.any_nan = 1;
         __syncthreads();
     }
+    // half-dimension A1 for this pass?  TW over the box of the frame's data
+    // and the pass's centroids (tail features), with an ulp-scale slack per
+    // feature for the rounding of the online moves
+    bool half = false;
+    float twh = 0.0f, te = 0.0f;
+    if constexpr (PRUNE) {
+        float tw = 0.0f, tn = 0.0f;
+#pragma unroll
+        for (int d = C::H; d < D; ++d) {
+            float lo = __uint_as_float(keybits(sh.xtlo[d])), hi = __uint_as_float(keybits(sh.xthi[d]));
+#pragma unroll
+            for (int w = 0; w < C::NWV; ++w) {
+                lo = fminf(lo, sh.ptlo[w][d]);
+                hi = fmaxf(hi, sh.pthi[w][d]);
+            }
+            const float mag = fmaxf(fabsf(lo), fabsf(hi));
+            const float wd = fadd(fsub(hi, lo), fadd(fmul(mag, 0x1p-20f), 1e-30f));
+            tw = fadd(tw, fmul(wd, wd));
+            tn = fadd(tn, fmul(mag, mag));
+        }
+        tw = fmul(tw, 1.0f + 0x1p-10f);
+        float mh = 0.0f;
+#pragma unroll
+        for (int w = 0; w < C::NWV; ++w) mh = fmaxf(mh, sh.cnmax_h[w]);
+        twh = fmul(tw, 0.5f);
+        te = fadd(twh, fmul(fmul(fmul(tn, 2.0f), C::EPSF), 1.0f + 0x1p-10f));
+        // worth it while the tail slack is a small part of eps's norm scale
+        half = !(tw != tw) && te <= fmul(fmul(mh, C::EPSF), 0.25f) && !uniform_int(sh.any_nan) && !no_half;
+    }
     if (uniform_int(sh.any_nan)) {
         // NaN centroids (yakmo 0/0 means) make ANN's early exits order dependent:
         // this pass runs in the generic kernel (gsc_kernels.hip)
@@ -1267,6 +1383,14 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             frp->xseq = (int)xp.seq;
         }
         break;
+    }
+    if (half) {  // the A1 bounds cover the first H features: H-norms for the bound and for eps's M
+#pragma unroll
+        for (int s = 0; s < SL; ++s) cn[s] = (dmask >> s) & 1u ? __builtin_inff() : norm2_x<C::H>(creg[s]);
+        cnmax = sh.cnmax_h[vwave];
+        __syncthreads();  // every wave has read sh.cnmax_h / sh.cnmax above
+        if (lane == 0) sh.cnmax[vwave] = cnmax;
+        __syncthreads();
     }
 
     // wave-0 state: update log (lane = entry, tag = commit iteration) + residual (lane 0)
@@ -1302,7 +1426,6 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         VPState vst;
         if (wave == 0 && has_p) vp_begin<C>(sh, P_buf, P_off, P_n, vq_a10, lane, lg_pos, lg_tag, vst);
         STAMP(0)
-        int kstep = 0;  // wave 0: chain steps taken
         // A1 of the queries in mask m, two per trip: one query's min-tree (a
         // dependent DPP chain) overlaps the other's distance FMAs
         auto a1_mask = [&](uint64_t m) {
@@ -1313,12 +1436,11 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 const int j1 = m ? __ffsll((long long)m) - 1 : j0;
                 if (m) m &= m - 1;
                 float dv0[SL], dv1[SL];
-                a1_dist_x2<D, SL>(creg, cn, sh.qm[cur_buf][j0], sh.qm[cur_buf][j1], dv0, dv1);
+                if (half)
+                    a1_dist_x2<C::H, D, SL>(creg, cn, sh.qm[cur_buf][j0], sh.qm[cur_buf][j1], dv0, dv1);
+                else
+                    a1_dist_x2<D, D, SL>(creg, cn, sh.qm[cur_buf][j0], sh.qm[cur_buf][j1], dv0, dv1);
                 a1_reduce2<C>(dv0, dv1, sh.wrec[vwave][j0], sh.wrec[vwave][j1], vwave, lane);
-                if (wave == 0 && has_p) {
-                    if (kstep < KB) vp_step<C>(kstep++, lane, lg_pos, vst);
-                    if (kstep < KB) vp_step<C>(kstep++, lane, lg_pos, vst);
-                }
             }
         };
         const uint64_t curm = cur_n > 0 ? (cur_n >= 64 ? ~0ull : (1ull << cur_n) - 1ull) : 0ull;
@@ -1329,11 +1451,12 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 const int jr = lane < cur_n ? lane : 0;
                 const float* qv = sh.q[cur_buf][jr];
                 lbp = wave_box_lb<C>(sh, qv, vwave);
-                qn_j = norm2_x<D>(qv);
+                qn_j = half ? norm2_x<C::H>(qv) : norm2_x<D>(qv);
                 float M = 0.0f;
 #pragma unroll
                 for (int w = 0; w < C::NWV; ++w) M = fmaxf(M, sh.cnmax[w]);
-                eps_j = fadd(fmul(fadd(qn_j, M), C::EPSF), 1e-37f);
+                eps_j = fadd(fadd(fmul(fadd(qn_j, M), C::EPSF), 1e-37f), te);
+                qn_j = fadd(qn_j, twh);  // |q_h|^2 + TW/2 in half-dimension passes
                 // home queries (q inside this wave's box) first: their minima bound
                 // the others (a query outside every box is evaluated by all waves)
                 const uint64_t home = __ballot(lbp == 0.0f) & curm;
@@ -1355,11 +1478,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         } else {
             a1_mask(curm);
         }
-        if (wave == 0 && has_p) {
-#pragma unroll 1
-            for (int k = kstep; k < KB; ++k) vp_step<C>(k, lane, lg_pos, vst);
-            vp_end<C>(sh, P_buf, P_off, P_n, lane, lg_pos, vst);
-        }
+        if (wave == 0 && has_p) vp_end<C>(sh, P_buf, P_off, P_n, lane, lg_pos, vst);
         STAMP(1)
         lds_barrier();
         STAMP(6)
@@ -1382,7 +1501,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             STAMP(8)
 #pragma unroll 1
             for (int j0 = wave * 4; j0 < cur_n; j0 += 4 * NWL)
-                a2_group<C, true>(sh, j0, cur_n, sh.q[cur_buf], sh.qrec[cur_buf], 0, nullptr, lane
+                a2_group<C, true>(sh, j0, cur_n, sh.q[cur_buf], sh.qrec[cur_buf], 0, nullptr, lane, half, twh, te
 #ifdef GSC_STAMPS
                                   , acc, &tlast
 #endif
@@ -1405,7 +1524,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                         const float lb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbp), jj));
                         if (lane == 0) sh.wrec[vwave][jj].minbits = __float_as_uint(lb);
                     } else {
-                        a1_query<C>(creg, sh.q[cur_buf][jj], sh.wrec[vwave][jj], vwave, lane);
+                        a1_query<C>(creg, sh.q[cur_buf][jj], sh.wrec[vwave][jj], vwave, lane, dmask);
                     }
                 }
                 lds_barrier();
@@ -1468,7 +1587,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             if (lastc) {
 #pragma unroll
                 for (int d = 0; d < D; ++d) sh.lg_c[tgt][d] = sh.newc[j][d];
-                sh.lg_c[tgt][C::ROW - 1] = norm2_x<D>(sh.newc[j]);
+                sh.lg_c[tgt][C::ROW - 1] = half ? norm2_x<C::H>(sh.newc[j]) : norm2_x<D>(sh.newc[j]);
                 sh.asg[tgt] = R.cstar;
             }
             wave_lds_sync();
@@ -1541,7 +1660,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             // the failed query on the live centroids: fresh distances and
             // certificate; exact DFS if the certificate still fails
             ++restarts;
-            a1_query<C>(creg, sh.qslow, sh.wrec[vwave][KB], vwave, lane);
+            a1_query<C>(creg, sh.qslow, sh.wrec[vwave][KB], vwave, lane, dmask);
             lds_barrier();
             if constexpr (NWG == 2) {
                 write_cstar<C>(sh, creg, &sh.qsolo, 1ull, KB, wave, lane, wg);
@@ -1576,7 +1695,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 }
 #pragma unroll
                 for (int s = 0; s < SL; ++s)
-                    if (p0 + s < K) sh.dist[p0 + s] = dv[s];
+                    if (p0 + s < K) sh.dist[p0 + s] = ((dmask >> s) & 1u) ? __builtin_inff() : dv[s];
                 if constexpr (NWG == 2) {  // the partner's half of the live distances
                     lds_barrier();
                     ++xp.seq;
@@ -1638,7 +1757,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                     lg_tag = it;
 #pragma unroll
                     for (int d = 0; d < D; ++d) sh.lg_c[e][d] = sh.solo_c[d];
-                    sh.lg_c[e][C::ROW - 1] = norm2_x<D>(sh.solo_c);
+                    sh.lg_c[e][C::ROW - 1] = half ? norm2_x<C::H>(sh.solo_c) : norm2_x<D>(sh.solo_c);
                 }
                 sh.pub_pos[lane] = lane == e ? bpos : -1;
             }
@@ -1663,15 +1782,17 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
 #pragma unroll
     for (int s = 0; s < SL; ++s) {
         const int p = p0 + s;
-        if (p < K) {
+        if (!((dmask >> s) & 1u)) {
             const int id = sh.t.pidx[p];
 #pragma unroll
             for (int d = 0; d < D; ++d) C_[(int64_t)id * D + d] = creg[s][d];
         }
     }
     if (wg0)
-        for (int p = tid; p < K; p += nthreads)  // the commits' atomics live in L2: read past this CU's L1
-            prev_cnt[sh.t.pidx[p]] = __hip_atomic_load(&cnta[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int p = tid; p < K; p += nthreads) {  // the commits' atomics live in L2: read past this CU's L1
+            const int id = sh.t.pidx[p];
+            if (id != 0xFFFF) prev_cnt[id] = __hip_atomic_load(&cnta[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
 #ifdef GSC_STAMPS
     if (lane == 0 && wg0)
         for (int k = 0; k < 16; ++k) frp->stamps[wave * 16 + k] += acc[k];
@@ -1719,7 +1840,8 @@ using namespace gsc;
 
 template <class C>
 static hipError_t launch_scan(ReduceFrame* frames, int nframes, const float* X, float* Cc, int* is,
-                              const float* rate_tab, double tol, int max_passes, uint64_t* xbuf, hipStream_t st) {
+                              const float* rate_tab, double tol, int max_passes, uint64_t* xbuf, int opts,
+                              hipStream_t st) {
     const size_t shm = sizeof(Scan2Shared<C>);
     static_assert(sizeof(Scan2Shared<C>) <= 160 * 1024, "LDS budget (160 KB per CU)");
     hipError_t e = hipFuncSetAttribute((const void*)scan_batch_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1727,7 +1849,7 @@ static hipError_t launch_scan(ReduceFrame* frames, int nframes, const float* X, 
     if (e != hipSuccess) return e;
     if constexpr (C::NWG == 1) {
         hipLaunchKernelGGL(scan_batch_kernel<C>, dim3(nframes), dim3(C::NT), shm, st, frames, nframes, X, Cc, is,
-                           rate_tab, tol, max_passes, xbuf);
+                           rate_tab, tol, max_passes, xbuf, opts);
         return hipGetLastError();
     } else {
         // both workgroups of a frame must be resident together: a cooperative
@@ -1737,13 +1859,14 @@ static hipError_t launch_scan(ReduceFrame* frames, int nframes, const float* X, 
         if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
         int pairs = std::min(nframes, std::max(1, cus / 2));
         if (pairs >= 8) pairs -= pairs % 8;  // whole groups of 16 workgroups: pair members share an XCD
-        void* args[] = {&frames, &nframes, &X, &Cc, &is, &rate_tab, &tol, &max_passes, &xbuf};
+        void* args[] = {&frames, &nframes, &X, &Cc, &is, &rate_tab, &tol, &max_passes, &xbuf, &opts};
         return hipLaunchCooperativeKernel((const void*)scan_batch_kernel<C>, dim3(2 * pairs), dim3(C::NT), args, shm,
                                           st);
     }
 }
 
-// Batched KNNScanReduce for every frame (K = 2^logk, 256..4096; D = 8 or 16,
+// Batched KNNScanReduce for every frame (K <= 2^logk, 2^logk in 256..4096; a
+// frame's own K (frp->K) below 2^logk runs the padded layout; D = 8 or 16,
 // and D = 32 with two CUs per frame at K = 4096): each frame runs its passes
 // from frp->iters until it converges, reaches max_passes or meets a NaN pass
 // (left to the generic kernel).  xbuf: 2 x 2 x 2048 zeroed granules per frame
@@ -1751,12 +1874,15 @@ static hipError_t launch_scan(ReduceFrame* frames, int nframes, const float* X, 
 // not cover.
 extern "C" hipError_t gsc_launch_scan_batch(int D, int logk, ReduceFrame* frames, int nframes, const float* X,
                                             float* Cc, int* is, const float* rate_tab, double tol, int max_passes,
-                                            uint64_t* xbuf, hipStream_t st) {
+                                            uint64_t* xbuf, int opts, hipStream_t st) {
 #define SB(DV, LK, SLV, NG)                                                                                    \
     if (D == DV && logk == LK)                                                                                 \
-        return launch_scan<ScanCfg<DV, LK, SLV, NG>>(frames, nframes, X, Cc, is, rate_tab, tol, max_passes, xbuf, st);
-    SB(8, 8, 8, 1) SB(8, 9, 8, 1) SB(8, 10, 8, 1) SB(8, 11, 8, 1) SB(8, 12, 8, 1)
-    SB(16, 8, 8, 1) SB(16, 9, 8, 1) SB(16, 10, 8, 1) SB(16, 11, 8, 1) SB(16, 12, 8, 1)
+        return launch_scan<ScanCfg<DV, LK, SLV, NG>>(frames, nframes, X, Cc, is, rate_tab, tol, max_passes, xbuf, \
+                                                     opts, st);
+    // K below 4096: four leaves per lane, so a frame gets twice the waves
+    // (K = 512: two instead of one); the per-search work there is latency
+    SB(8, 8, 4, 1) SB(8, 9, 4, 1) SB(8, 10, 4, 1) SB(8, 11, 4, 1) SB(8, 12, 8, 1)
+    SB(16, 8, 4, 1) SB(16, 9, 4, 1) SB(16, 10, 4, 1) SB(16, 11, 4, 1) SB(16, 12, 8, 1)
     SB(32, 8, 4, 1) SB(32, 9, 4, 1) SB(32, 10, 4, 1) SB(32, 11, 4, 1) SB(32, 12, 4, 2)
 #undef SB
     return hipErrorInvalidValue;

@@ -234,6 +234,53 @@ __device__ __forceinline__ void node_segment(int h, int K, int& s, int& n, int& 
     }
 }
 
+// Embeds ANN's tree over kr points (build_tree: heap-indexed, n_lo = n/2,
+// compact leaf positions 0..kr-1) into the complete tree of 2^LOGK leaves the
+// batched kernel lays out in registers: node h keeps its heap index (the same
+// root path); a point's leaf position is its root path over LOGK levels,
+// continuing below its own leaf the way node_segment does (a node of one
+// point hands it to its high child).  Those nodes below a point (n <= 1)
+// become pass-through splits that send every query to the high child
+// (cut value -inf, cell [-inf, inf]): ANN's search and the padded one reach
+// the real leaves in the same order under the same conditions, and the
+// padding leaves (pidx 0xFFFF) carry +inf distances, so they are never a
+// result and never an improvement.  stage: kr ints of scratch.
+template <int LOGK>
+__device__ void pad_tree(KdTree& t, int* __restrict__ stage, int kr, int tid, int nt) {
+    constexpr int K = 1 << LOGK;
+    __syncthreads();  // build_tree is done with the scratch
+    for (int i = tid; i < kr; i += nt) stage[i] = t.pidx[i];
+    __syncthreads();
+    for (int p = tid; p < K; p += nt) t.pidx[p] = 0xFFFF;
+    __syncthreads();
+    for (int i = tid; i < kr; i += nt) {
+        int s = 0, n = kr, pos = 0;
+        for (int l = 0; l < LOGK; ++l) {
+            const int half = n >> 1;
+            const int hi = i >= s + half ? 1 : 0;
+            if (hi) {
+                s += half;
+                n -= half;
+            } else {
+                n = half;
+            }
+            pos = (pos << 1) | hi;
+        }
+        t.pidx[pos] = (uint16_t)stage[i];
+    }
+    for (int h = tid; h < K - 1; h += nt) {
+        int s, n, depth;
+        node_segment(h, kr, s, n, depth);
+        if (n <= 1) {
+            t.cd[h] = 0;
+            t.cv[h] = -__builtin_inff();
+            t.lo[h] = -__builtin_inff();
+            t.hi[h] = __builtin_inff();
+        }
+    }
+    __syncthreads();
+}
+
 template <int D>
 __device__ void build_tree(KdTree& sh, float* __restrict__ scratch, const float* __restrict__ C, int K) {
     const int tid = threadIdx.x;

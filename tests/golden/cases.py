@@ -84,6 +84,10 @@ CASES = {
     # C5: 48 kHz stereo at ChunkCount 4096, the encoder default ChunkSize 4 and 8
     "syn8s_48k_cs4_cpf4096": (lambda: _synth(8.0, 48000), ["-cs4", "-cpf4096"]),
     "syn8s_48k_cs8_cpf4096": (lambda: _synth(8.0, 48000), ["-cs8", "-cpf4096"]),
+    # the reference's own -br invocations (encoder/encoder.lps:270-279): ChunksPerFrame from the bit-rate
+    # cost loop (encoder.lpr:1337-1351) -- K = 485 and 1852 here, not powers of two
+    "syn8s_br128_vfr05_cs8": (lambda: _synth(8.0), ["-br128", "-vfr0.5", "-cs8"]),
+    "syn8s_br128_vfr05_cs16": (lambda: _synth(8.0), ["-br128", "-vfr0.5", "-cs16"]),
 }
 
 
