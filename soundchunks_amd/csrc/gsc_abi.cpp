@@ -24,7 +24,7 @@
 extern "C" hipError_t gsc_launch_yakmo(int D, const gsc::ReduceFrame* frames, int nframes, const float* X, float* C,
                                        float* fs, int* is, uint32_t* bits, int max_n, hipStream_t st);
 extern "C" hipError_t gsc_launch_ann_build(const float* pts, int n, int dd, int* pidx, int* cd, float* cv, float* lo,
-                                           float* hi, float* bnd, hipStream_t st);
+                                           float* hi, float* bnd, float* val, hipStream_t st);
 extern "C" hipError_t gsc_launch_ann_query(const float* pts, int n, int dd, int* pidx, int* cd, float* cv, float* lo,
                                            float* hi, float* bnd, const float* q, int k, int mode, float eps,
                                            int* idxs, float* errs, float* dist, float* mk_key, int* mk_info,
@@ -230,7 +230,7 @@ ann_kdtree_t* ann_kdtree_create(float** pa, int n, int dd, int bs, int split) {
     if (n > 0) {
         stage_points(t, nullptr, fn);
         if ((e = gsc_launch_ann_build(t->d_pts, n, dd, t->d_pidx, t->d_cd, t->d_cv, t->d_lo, t->d_hi, t->d_bnd,
-                                      nullptr)) != hipSuccess)
+                                      t->d_dist, nullptr)) != hipSuccess)
             return give_up("tree build launch", e);
         if ((e = hipDeviceSynchronize()) != hipSuccess) return give_up("tree build", e);
     }

@@ -2,8 +2,8 @@
 // (ann_kdtree_create / _search / _pri_search / _search_multi /
 // _pri_search_multi).  The encoder itself uses the batched kernels in
 // gsc_kernels.hip; this file serves the per-query drop-in ABI, so it favours
-// exactness over speed: one lane runs ANN 1.1's sequential build (ANN.dll
-// @0x180014620 ctor); a search computes every live point distance with all
+// exactness over speed: one workgroup builds the tree level by level with
+// ANN 1.1's own split code per node (ANN.dll @0x180014620 ctor); a search computes every live point distance with all
 // lanes of one workgroup and then walks ANN's DFS (@0x1800124b0 annkSearch)
 // or best-bin-first search (@0x180011da0 annkPriSearch) on one lane.
 #include <hip/hip_runtime.h>
@@ -21,21 +21,45 @@ __device__ __forceinline__ float fa(float a, float b) { return __fadd_rn(a, b); 
 __device__ __forceinline__ float fs(float a, float b) { return __fsub_rn(a, b); }
 __device__ __forceinline__ float fm(float a, float b) { return __fmul_rn(a, b); }
 
-#define PA(i, d) (t.pts[(int64_t)pidx[(i)] * t.dd + (d)])
+// ---------------------------------------------------------------------------
+// ANNkd_tree ctor with ANN_KD_STD, bs = 1 (ANN.dll @0x180014620): annEnclRect,
+// then rkd_tree with kd_split = annMaxSpread + annMedianSplit (@0x180015260,
+// @0x180015680), built level by level by one workgroup.  The nodes of a level
+// own disjoint segments of pidx, so they split independently; within a node
+// the reference's sequential quickselect runs unchanged on one lane (its
+// swap order decides the leaf order among tied values, which the KNNFit
+// overflow replay depends on), over the segment's cut values staged in a
+// contiguous scratch array instead of the pidx -> pts gathers.  annMaxSpread
+// is a min / max per dimension: "if (c < mn) mn = c; else if (c > mx) mx = c"
+// from the segment's first point equals the NaN-ignoring min / max, except
+// that a NaN first value stays NaN -- so long segments (>= kWaveSeg) reduce
+// it over a wave's lanes.  Short ones run one node per lane.
+// ---------------------------------------------------------------------------
+constexpr int kBuildThreads = 256;
+constexpr int kWaveSeg = 512;
 
-__device__ void median_split(const Tree& t, int* pidx, int n, int d, float* cv, int n_lo) {
+// annMedianSplit on (pidx, val) of one segment; returns the cut value
+__device__ float median_split_v(int* __restrict__ pidx, float* __restrict__ val, int n, int n_lo) {
     int l = 0, r = n - 1;
-#define SWP(a, b) { const int x_ = pidx[a]; pidx[a] = pidx[b]; pidx[b] = x_; }
+#define SWP(a, b)                   \
+    {                               \
+        const int x_ = pidx[a];     \
+        pidx[a] = pidx[b];          \
+        pidx[b] = x_;               \
+        const float v_ = val[a];    \
+        val[a] = val[b];            \
+        val[b] = v_;                \
+    }
     while (l < r) {
         int i = (r + l) / 2, k;
-        if (PA(i, d) > PA(r, d)) SWP(i, r)
+        if (val[i] > val[r]) SWP(i, r)
         SWP(l, i);
-        const float c = PA(l, d);
+        const float c = val[l];
         i = l;
         k = r;
         for (;;) {
-            while (PA(++i, d) < c) {}
-            while (PA(--k, d) > c) {}
+            while (val[++i] < c) {}
+            while (val[--k] > c) {}
             if (i < k) SWP(i, k) else break;
         }
         SWP(l, k);
@@ -44,91 +68,139 @@ __device__ void median_split(const Tree& t, int* pidx, int n, int d, float* cv, 
         else break;
     }
     if (n_lo > 0) {
-        float c = PA(0, d);
+        float c = val[0];
         int k = 0;
         for (int i = 1; i < n_lo; ++i)
-            if (PA(i, d) > c) { c = PA(i, d); k = i; }
+            if (val[i] > c) { c = val[i]; k = i; }
         SWP(n_lo - 1, k);
     }
 #undef SWP
-    *cv = (float)((double)fa(PA(n_lo - 1, d), PA(n_lo, d)) / 2.0);
+    return (float)((double)fa(val[n_lo - 1], val[n_lo]) / 2.0);
 }
 
-// ANNkd_tree ctor with ANN_KD_STD, bs = 1: annEnclRect, then rkd_tree with
-// kd_split (annMaxSpread + annMedianSplit) -- iterative pre-order
-__device__ void build_seq(const Tree& t) {
+// segment [s, s + m) of heap node h at depth `depth` (n_lo = m / 2)
+__device__ __forceinline__ void ann_segment(int h, int n, int depth, int& s, int& m) {
+    const int path = h + 1;
+    s = 0;
+    m = n;
+    for (int bl = depth - 1; bl >= 0; --bl) {
+        const int half = m >> 1;
+        if ((path >> bl) & 1) { s += half; m -= half; }
+        else m = half;
+    }
+}
+
+// split node h (spread already reduced to cdim): quickselect, cut value, cell
+// bounds on cdim (root rect narrowed by ancestors cutting the same dimension)
+__device__ void finish_node(const Tree& t, int h, int depth, int s, int m, int cdim) {
+    const int n_lo = m / 2;
+    const float cvv = median_split_v(t.pidx + s, t.val + s, m, n_lo);
+    float lov = t.bnd[cdim], hiv = t.bnd[t.dd + cdim];
+    int a = 0;
+    const int path = h + 1;
+    for (int bl = depth - 1; bl >= 0; --bl) {
+        const int right = (path >> bl) & 1;
+        if (t.cd[a] == cdim) {
+            if (right) lov = t.cv[a];
+            else hiv = t.cv[a];
+        }
+        a = 2 * a + 1 + right;
+    }
+    t.cd[h] = cdim;
+    t.cv[h] = cvv;
+    t.lo[h] = lov;
+    t.hi[h] = hiv;
+}
+
+__device__ __forceinline__ float wave_fmin(float v) {
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float wave_fmax(float v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+
+__device__ void build_par(const Tree& t) {
     const int n = t.n, dd = t.dd;
-    for (int i = 0; i < n; ++i) t.pidx[i] = i;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
     int* pidx = t.pidx;
-    for (int d = 0; d < dd; ++d) {
-        float lo = PA(0, d), hi = PA(0, d);
-        for (int i = 0; i < n; ++i) {
-            const float v = PA(i, d);
-            if (v < lo) lo = v;
-            else if (v > hi) hi = v;
-        }
-        t.bnd[d] = lo;
-        t.bnd[dd + d] = hi;
-    }
-    // explicit stack of (heap index, segment start, size); bounds per node are
-    // the root rect narrowed by ancestors cutting the same dimension
-    int st_h[64], st_s[64], st_n[64];
-    int sp = 0;
-    st_h[0] = 0; st_s[0] = 0; st_n[0] = n; sp = 1;
-    while (sp > 0) {
-        --sp;
-        const int h = st_h[sp], s = st_s[sp], m = st_n[sp];
-        if (m < 2) continue;
-        int* seg = t.pidx + s;
-        int cdim = 0;
-        float max_spr = 0.0f;
-        for (int d = 0; d < dd; ++d) {
-            float mn = t.pts[(int64_t)seg[0] * dd + d], mx = mn;
-            for (int i = 1; i < m; ++i) {
-                const float c = t.pts[(int64_t)seg[i] * dd + d];
-                if (c < mn) mn = c;
-                else if (c > mx) mx = c;
-            }
-            const float spr = fs(mx, mn);
-            if (spr > max_spr) { max_spr = spr; cdim = d; }
-        }
-        const int n_lo = m / 2;
-        float cvv;
-        median_split(t, seg, m, cdim, &cvv, n_lo);
-        float lov = t.bnd[cdim], hiv = t.bnd[dd + cdim];
-        {
-            int a = 0;
-            const int path = h + 1;
-            const int depth = 31 - __clz(path);
-            for (int bl = depth - 1; bl >= 0; --bl) {
-                const int right = (path >> bl) & 1;
-                if (t.cd[a] == cdim) {
-                    if (right) lov = t.cv[a];
-                    else hiv = t.cv[a];
+    for (int i = tid; i < n; i += blockDim.x) pidx[i] = i;
+    __syncthreads();
+    int depth = 0;
+    for (int sz = n; sz >= 2; sz -= sz >> 1, ++depth) {  // sz: the level's largest segment
+        const int first = (1 << depth) - 1, count = 1 << depth;
+        if (sz >= kWaveSeg) {  // one wave per node
+            for (int node = wave; node < count; node += nw) {
+                const int h = first + node;
+                int s, m;
+                ann_segment(h, n, depth, s, m);
+                if (m < 2) continue;
+                const int* seg = pidx + s;
+                int cdim = 0;
+                float max_spr = 0.0f;
+                for (int d = 0; d < dd; ++d) {
+                    float mn = __builtin_nanf(""), mx = __builtin_nanf("");
+                    for (int i = lane; i < m; i += 64) {
+                        const float c = t.pts[(int64_t)seg[i] * dd + d];
+                        mn = fminf(mn, c);
+                        mx = fmaxf(mx, c);
+                    }
+                    mn = wave_fmin(mn);
+                    mx = wave_fmax(mx);
+                    const float c0 = t.pts[(int64_t)seg[0] * dd + d];
+                    if (c0 != c0) mn = mx = c0;  // a NaN first value never moves
+                    const float spr = fs(mx, mn);
+                    if (spr > max_spr) { max_spr = spr; cdim = d; }
+                    if (h == 0 && lane == 0) {  // annEnclRect
+                        t.bnd[d] = mn;
+                        t.bnd[dd + d] = mx;
+                    }
                 }
-                a = 2 * a + 1 + right;
+                for (int i = lane; i < m; i += 64) t.val[s + i] = t.pts[(int64_t)seg[i] * dd + cdim];
+                __threadfence_block();  // the staged values (and bnd) before lane 0 reads them
+                if (lane == 0) finish_node(t, h, depth, s, m, cdim);
+            }
+        } else {  // one lane per node, the reference's loops
+            for (int node = tid; node < count; node += blockDim.x) {
+                const int h = first + node;
+                int s, m;
+                ann_segment(h, n, depth, s, m);
+                if (m < 2) continue;
+                const int* seg = pidx + s;
+                int cdim = 0;
+                float max_spr = 0.0f;
+                for (int d = 0; d < dd; ++d) {
+                    float mn = t.pts[(int64_t)seg[0] * dd + d], mx = mn;
+                    for (int i = 1; i < m; ++i) {
+                        const float c = t.pts[(int64_t)seg[i] * dd + d];
+                        if (c < mn) mn = c;
+                        else if (c > mx) mx = c;
+                    }
+                    const float spr = fs(mx, mn);
+                    if (spr > max_spr) { max_spr = spr; cdim = d; }
+                    if (h == 0) {
+                        t.bnd[d] = mn;
+                        t.bnd[dd + d] = mx;
+                    }
+                }
+                for (int i = 0; i < m; ++i) t.val[s + i] = t.pts[(int64_t)seg[i] * dd + cdim];
+                finish_node(t, h, depth, s, m, cdim);
             }
         }
-        t.cd[h] = cdim;
-        t.cv[h] = cvv;
-        t.lo[h] = lov;
-        t.hi[h] = hiv;
-        // pre-order: push hi first so lo is processed first
-        st_h[sp] = 2 * h + 2; st_s[sp] = s + n_lo; st_n[sp] = m - n_lo; ++sp;
-        st_h[sp] = 2 * h + 1; st_s[sp] = s; st_n[sp] = n_lo; ++sp;
+        __syncthreads();
+    }
+    if (n == 1 && tid < dd) {  // annEnclRect of a single point (no split node)
+        t.bnd[tid] = t.pts[tid];
+        t.bnd[dd + tid] = t.pts[tid];
     }
 }
-#undef PA
 
-__global__ void build_kernel(Tree t) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    build_seq(t);
-}
+__global__ __launch_bounds__(kBuildThreads) void build_kernel(Tree t) { build_par(t); }
 
-// one tree per block (lane 0): the KNNFit candidate trees of several frames
-__global__ void build_many_kernel(const Tree* __restrict__ trees) {
-    if (threadIdx.x != 0) return;
-    build_seq(trees[blockIdx.x]);
+// one tree per workgroup: the KNNFit candidate trees of several frames
+__global__ __launch_bounds__(kBuildThreads) void build_many_kernel(const Tree* __restrict__ trees) {
+    build_par(trees[blockIdx.x]);
 }
 
 struct MinK {
@@ -422,10 +494,11 @@ __global__ __launch_bounds__(kOvBlock) void knnfit_ann_kernel(const Tree* __rest
 }  // namespace ann
 }  // namespace gsc
 
+// val: n floats of scratch
 extern "C" hipError_t gsc_launch_ann_build(const float* pts, int n, int dd, int* pidx, int* cd, float* cv, float* lo,
-                                           float* hi, float* bnd, hipStream_t st) {
-    gsc::ann::Tree t{pts, n, dd, pidx, cd, cv, lo, hi, bnd};
-    hipLaunchKernelGGL(gsc::ann::build_kernel, dim3(1), dim3(64), 0, st, t);
+                                           float* hi, float* bnd, float* val, hipStream_t st) {
+    gsc::ann::Tree t{pts, n, dd, pidx, cd, cv, lo, hi, bnd, val};
+    hipLaunchKernelGGL(gsc::ann::build_kernel, dim3(1), dim3(gsc::ann::kBuildThreads), 0, st, t);
     return hipGetLastError();
 }
 
@@ -433,7 +506,7 @@ extern "C" hipError_t gsc_launch_ann_query(const float* pts, int n, int dd, int*
                                            float* hi, float* bnd, const float* q, int k, int mode, float eps, int* idxs,
                                            float* errs, float* dist, float* mk_key, int* mk_info, float* pq_key,
                                            int* pq_h, int* pq_s, int* pq_n, hipStream_t st) {
-    gsc::ann::Tree t{pts, n, dd, pidx, cd, cv, lo, hi, bnd};
+    gsc::ann::Tree t{pts, n, dd, pidx, cd, cv, lo, hi, bnd, nullptr};
     hipLaunchKernelGGL(gsc::ann::query_kernel, dim3(1), dim3(1024), 0, st, t, q, k, mode, eps, idxs, errs, dist, mk_key,
                        mk_info, pq_key, pq_h, pq_s, pq_n);
     return hipGetLastError();
@@ -441,7 +514,7 @@ extern "C" hipError_t gsc_launch_ann_query(const float* pts, int n, int dd, int*
 
 // trees: device array of ntrees descriptors (their arrays already allocated)
 extern "C" hipError_t gsc_launch_ann_build_many(const void* trees, int ntrees, hipStream_t st) {
-    hipLaunchKernelGGL(gsc::ann::build_many_kernel, dim3(ntrees), dim3(64), 0, st,
+    hipLaunchKernelGGL(gsc::ann::build_many_kernel, dim3(ntrees), dim3(gsc::ann::kBuildThreads), 0, st,
                        static_cast<const gsc::ann::Tree*>(trees));
     return hipGetLastError();
 }

@@ -21,6 +21,7 @@ struct ReduceFrame {
     int64_t n_off;        // per-point scratch (N): clusters, d0, id, cum at +n_off
     int64_t k_off;        // per-centroid scratch (K): previous-pass counts by centroid id
     int64_t ka_off;       // per-centroid scratch (K): this pass's counts by kd-leaf position
+    int64_t t_off;        // split layout (D = 32, K = 4096): the tail features, K x 16 floats at T + t_off
     int32_t N, K;
     int32_t iters;        // out: KNNScanReduce passes
     int32_t slow;         // out: searches resolved by the exact DFS fallback
@@ -30,7 +31,7 @@ struct ReduceFrame {
     int32_t restarts;     // out: batched-pipeline restarts (diagnostic)
     int32_t loop_iters;   // out: batched-pipeline iterations (diagnostic); -1 = guard tripped
     int32_t tree_exact;   // out: passes whose kd-tree needed the sequential build (median ties)
-    int32_t xseq;         // two-CU frames (D = 32, K = 4096): tag of the last hand-off between the two CUs
+    int32_t xseq;         // two-CU frames: tag of the last hand-off between the two CUs
     uint64_t t_done;      // out: s_memrealtime (100 MHz) when the batched kernel finished the frame
     // optional (batched kernel): when the frame is done, its final clusters are
     // copied to cl_host (host-mapped, N ints) and then *notify is set (system
@@ -97,6 +98,7 @@ struct AnnTree {
     float* lo;
     float* hi;
     float* bnd;        // 2 * dd: bounding rect lo | hi
+    float* val;        // n floats of build scratch (the staged cut values)
 };
 
 // One KNNFit query whose tie set exceeds ANN's 64-NN bucket: replayed through

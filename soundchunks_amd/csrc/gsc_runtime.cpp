@@ -31,8 +31,9 @@ extern "C" hipError_t gsc_launch_scan_pass(int D, gsc::ReduceFrame* frames, int 
                                            int only_flagged, hipStream_t st);
 extern "C" hipError_t gsc_launch_scan_batch(int D, int logk, gsc::ReduceFrame* frames, int nframes, const float* X,
                                             float* C, int* is, const float* rate_tab, double tol, int max_passes,
-                                            uint64_t* xbuf, int opts, hipStream_t st);
+                                            uint64_t* xbuf, int opts, float* tails, hipStream_t st);
 extern "C" size_t gsc_scan_xbuf_granules_per_frame(void);
+extern "C" size_t gsc_scan_tail_floats_per_frame(int D, int logk);
 extern "C" hipError_t gsc_launch_atten(int cs, gsc::DspFrame* frames, int nframes, const double* samp, int64_t span,
                                        int ch, int obd, hipStream_t st);
 extern "C" hipError_t gsc_launch_features(int cs, const gsc::DspFrame* frames, int nframes, int max_n,
@@ -118,9 +119,10 @@ int ensure_device() {
         } else {
             hipDeviceProp_t p;
             int dev = 0;
-            hipGetDevice(&dev);
-            hipGetDeviceProperties(&p, dev);
-            if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0) {
+            if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) {
+                why = "cannot query the HIP device";
+                state = -1;
+            } else if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0) {
                 why = std::string("device is ") + p.gcnArchName + ", kernels are built for gfx950 only";
                 state = -1;
             } else {
@@ -185,17 +187,19 @@ int padded_k(int K) {
 }
 
 // D in {8, 16, 32} and 2 <= K <= 4096: the batched speculative kernel
-// (gsc_scan.hip) covers the pass (K = 4096 at D = 32 on two CUs per frame,
-// which has no padded form: D = 32 with 2048 < K < 4096 runs the generic kernel).
+// (gsc_scan.hip) covers the pass (D = 32 with 2048 < K <= 4096 on one CU per
+// frame in the split layout: the cepstrum half of each centroid in HBM).
 bool batched_scan_shape(int D, int K) {
     if (std::getenv("GSC_SCAN_GENERIC")) return false;  // diagnostic switch
-    if (!(D == 8 || D == 16 || D == 32) || K < 2 || K > 4096) return false;
-    return !(D == 32 && K > 2048 && K != 4096);
+    return (D == 8 || D == 16 || D == 32) && K >= 2 && K <= 4096;
 }
 
-// D = 32 at K = 4096 runs each frame on two CUs, which hand data over through
-// zeroed per-frame granule slots
-bool two_cu_frames(int D, int K) { return D == 32 && K == 4096; }
+// no batched shape runs a frame on two CUs any more (the kernel keeps the
+// hand-off protocol for a future wide shape; xbuf stays unallocated)
+bool two_cu_frames(int, int) { return false; }
+
+// split-layout tail array offset of frame i (frames' slots of the largest size)
+int64_t tail_offset(int i) { return int64_t(i) * 4096 * 16; }
 
 // launch rounds of launch_scan_passes since the last reset (bench: launches
 // of the dominant kernel)
@@ -217,6 +221,11 @@ hipError_t launch_scan_passes(int D, ReduceFrame* dfr, int nf, int K, const floa
     }
     int logk = 0;
     while ((1 << logk) < padded_k(K)) ++logk;
+    DevBuf<float> tails;  // split layout: every frame's tail features (ReduceFrame::t_off)
+    if (batched && gsc_scan_tail_floats_per_frame(D, logk) > 0) {
+        const hipError_t e = tails.alloc(size_t(tail_offset(nf)));
+        if (e != hipSuccess) return e;
+    }
     int max_passes = kMaxScanIters;
     if (const char* e = std::getenv("GSC_SCAN_MAX_PASSES")) max_passes = std::max(1, std::min(kMaxScanIters, std::atoi(e)));
     // every launch advances each live frame by at least one pass (the batched
@@ -228,7 +237,7 @@ hipError_t launch_scan_passes(int D, ReduceFrame* dfr, int nf, int K, const floa
             // opts bit 0 (diagnostic GSC_SCAN_FULL_A1): full-dimension A1 bounds in every pass
             const int opts = std::getenv("GSC_SCAN_FULL_A1") ? 1 : 0;
             const hipError_t e =
-                gsc_launch_scan_batch(D, logk, dfr, nf, X, C, is, rate, tol, max_passes, xbuf.p, opts, nullptr);
+                gsc_launch_scan_batch(D, logk, dfr, nf, X, C, is, rate, tol, max_passes, xbuf.p, opts, tails.p, nullptr);
             if (e != hipSuccess) return e;
         }
         const hipError_t e = gsc_launch_scan_pass(D, dfr, nf, K, X, C, is, fs, rate, tol, max_passes, batched ? 1 : 0, nullptr);
@@ -287,6 +296,7 @@ int run_reduce_batch_dev(int D, int K, int precision, const std::vector<int>& Ns
     for (int i = 0; i < nf; ++i) {
         fr[i].k_off = no + int64_t(i) * K;
         fr[i].ka_off = no + int64_t(nf) * K + int64_t(i) * Kp;
+        fr[i].t_off = tail_offset(i);
         if (cl_host && notify) {
             fr[i].cl_host = cl_host + fr[i].n_off;
             fr[i].notify = notify + i;
@@ -316,13 +326,13 @@ int run_reduce_batch_dev(int D, int K, int precision, const std::vector<int>& Ns
     HIP_TRY(hipEventRecord(e2, nullptr));
     HIP_TRY(hipEventSynchronize(e2));
     float t1 = 0, t2 = 0;
-    hipEventElapsedTime(&t1, e0, e1);
-    hipEventElapsedTime(&t2, e1, e2);
+    (void)hipEventElapsedTime(&t1, e0, e1);
+    (void)hipEventElapsedTime(&t2, e1, e2);
     if (yakmo_ms) *yakmo_ms += t1;
     if (scan_ms) *scan_ms += t2;
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
-    hipEventDestroy(e2);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipEventDestroy(e2);
     C->resize(size_t(nf) * K * D);
     clusters->resize(size_t(no));
     HIP_TRY(hipMemcpy(C->data(), dC.p, sizeof(float) * C->size(), hipMemcpyDeviceToHost));
@@ -387,6 +397,7 @@ int run_knnfit_overflow(int CS, const std::vector<FitFrame>& fr, const std::vect
                         const std::vector<float>& eps, const std::vector<float>& cand, const std::vector<float>& q,
                         std::vector<int>* best, hipStream_t st) {
     const int nt = int(ov_frames.size());
+    const double t_begin = now_ms();
     std::vector<float> pts;
     std::vector<int64_t> pt_off(static_cast<size_t>(nt)), nd_off(static_cast<size_t>(nt));
     std::vector<int> caps(static_cast<size_t>(nt));
@@ -431,13 +442,14 @@ int run_knnfit_overflow(int CS, const std::vector<FitFrame>& fr, const std::vect
     if (q.size() > size_t(INT32_MAX)) return fail("KNNFit overflow: query slab exceeds 2^31 floats");
     // stream-ordered buffers: the replay runs on the caller's stream (the
     // post-processing stream during the scan) and never syncs the device
-    StreamBuf<float> dPts(st), dCv(st), dLo(st), dHi(st), dBnd(st), dQ(st), dPqk(st);
+    StreamBuf<float> dPts(st), dCv(st), dLo(st), dHi(st), dBnd(st), dQ(st), dPqk(st), dVal(st);
     StreamBuf<int> dPidx(st), dCd(st), dOut(st);
     StreamBuf<AnnTree> dTrees(st);
     StreamBuf<KnnOvJob> dJobs(st);
     StreamBuf<int4> dPqn(st);
     HIP_TRY(dPts.alloc(pts.size()));
     HIP_TRY(dPidx.alloc(size_t(pts.size() / size_t(CS))));
+    HIP_TRY(dVal.alloc(size_t(pts.size() / size_t(CS))));
     HIP_TRY(dCd.alloc(size_t(nodes)));
     HIP_TRY(dCv.alloc(size_t(nodes)));
     HIP_TRY(dLo.alloc(size_t(nodes)));
@@ -462,9 +474,18 @@ int run_knnfit_overflow(int CS, const std::vector<FitFrame>& fr, const std::vect
         a.lo = dLo.p + nd_off[t];
         a.hi = dHi.p + nd_off[t];
         a.bnd = dBnd.p + size_t(2 * CS) * size_t(t);
+        a.val = dVal.p + pt_off[t] / CS;
     }
     HIP_TRY(hipMemcpyAsync(dTrees.p, trees.data(), sizeof(AnnTree) * size_t(nt), hipMemcpyHostToDevice, st));
+    const bool timing = std::getenv("GSC_HOST_TIMING") != nullptr;
+    hipEvent_t eb0 = nullptr, eb1 = nullptr;
+    if (timing) {
+        HIP_TRY(hipEventCreate(&eb0));
+        HIP_TRY(hipEventCreate(&eb1));
+        HIP_TRY(hipEventRecord(eb0, st));
+    }
     HIP_TRY(gsc_launch_ann_build_many(dTrees.p, nt, st));
+    if (timing) HIP_TRY(hipEventRecord(eb1, st));
     // the box queues (<= one push per split node each): bounded launches
     const int pq_cap = max_n + 2;
     const size_t per_job = size_t(pq_cap) * (sizeof(float) + sizeof(int4));
@@ -479,6 +500,14 @@ int run_knnfit_overflow(int CS, const std::vector<FitFrame>& fr, const std::vect
     }
     HIP_TRY(hipMemcpyAsync(best->data(), dOut.p, sizeof(int) * best->size(), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    if (timing) {
+        float bms = 0.0f;
+        (void)hipEventElapsedTime(&bms, eb0, eb1);
+        (void)hipEventDestroy(eb0);
+        (void)hipEventDestroy(eb1);
+        std::fprintf(stderr, "KNNFit overflow: %d trees (largest %d candidates), %zu queries, %.2f ms (tree builds %.2f ms)\n",
+                     nt, max_n, jobs.size(), now_ms() - t_begin, double(bms));
+    }
     for (const KnnOvJob& j : jobs)
         if ((*best)[size_t(j.out)] < 0) return fail("KNNFit: ANN priority search emulation failed");
     return 0;
@@ -527,10 +556,10 @@ int run_knnfit_batch(int CS, const std::vector<int>& Rs, const std::vector<int>&
     HIP_TRY(hipEventRecord(e1, nullptr));
     HIP_TRY(hipEventSynchronize(e1));
     float t = 0;
-    hipEventElapsedTime(&t, e0, e1);
+    (void)hipEventElapsedTime(&t, e0, e1);
     if (knn_ms) *knn_ms += t;
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
     best->resize(size_t(qo / CS));
     HIP_TRY(hipMemcpy(best->data(), dOut.p, sizeof(int) * best->size(), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(fr.data(), dFr.p, sizeof(FitFrame) * size_t(nf), hipMemcpyDeviceToHost));

@@ -59,9 +59,14 @@
 namespace gsc {
 
 // Shape of one KNNScanReduce pipeline instance.
-template <int D_, int LOGK_, int SL_, int NWG_>
+template <int D_, int LOGK_, int SL_, int NWG_, int DR_ = D_>
 struct ScanCfg {
     static constexpr int D = D_, LOGK = LOGK_, SL = SL_, NWG = NWG_;
+    // features held in VGPRs; the other TL (split layout: the cepstrum half)
+    // live in a per-frame, position-indexed HBM array that only the lane owning
+    // the position reads and writes
+    static constexpr int DR = DR_, TL = D_ - DR_;
+    static constexpr bool SPLIT = TL > 0;
     static constexpr int K = 1 << LOGK;
     static constexpr int LS = SL == 8 ? 3 : (SL == 4 ? 2 : 1);        // log2 slots per lane
     static constexpr int LPW = 64 * SL;                                 // leaves per wave
@@ -81,6 +86,7 @@ struct ScanCfg {
     static_assert(NWV <= 16, "A2 evaluates up to 16 wave records per query (one per lane of a 16-lane group)");
     static_assert(KB <= 32 && 64 % KB == 0, "batch size");
     static_assert(NWG == 1 || (FULL && NWL == 8), "two-CU frames: 8 full waves per workgroup");
+    static_assert(!SPLIT || (NWG == 1 && DR == H), "split layout: one CU, the DCT half in registers");
 };
 
 // float minimum on f32 bit patterns (A1 values may be negative: the batch
@@ -376,10 +382,17 @@ __device__ __forceinline__ int wave_max_i(int v) {
 
 // pass start: the box of this wave's leaves
 template <class C>
-__device__ __forceinline__ void wave_box_init(Scan2Shared<C>& sh, const float (&creg)[C::SL][C::D], int vwave, int lane,
+__device__ __forceinline__ void wave_box_init(Scan2Shared<C>& sh, const float (&creg)[C::SL][C::DR], int vwave, int lane,
                                               int p0, uint32_t dmask) {
+    if constexpr (C::SPLIT) {  // the tail features: the pass setup's per-wave tail box
+        if (lane == 0)
+            for (int d = C::DR; d < C::D; ++d) {
+                sh.wlo[vwave][d] = sh.ptlo[vwave][d];
+                sh.whi[vwave][d] = sh.pthi[vwave][d];
+            }
+    }
 #pragma unroll  // static register indices: a runtime d would demote creg to scratch
-    for (int d = 0; d < C::D; ++d) {
+    for (int d = 0; d < C::DR; ++d) {
         float lo = __builtin_inff(), hi = -__builtin_inff();
 #pragma unroll
         for (int s = 0; s < C::SL; ++s)
@@ -505,11 +518,59 @@ __device__ __forceinline__ void a1_reduce2(const float (&dv0)[C::SL], const floa
     a1_store<C::SL>(t1, rec1, lane);
 }
 
+// max over the wave of a non-negative float (bit order = value order)
+__device__ __forceinline__ float wave_max_nonneg(float x) {
+    uint32_t k = __float_as_uint(x);
+    k = max(k, partner<0>(k));
+    k = max(k, partner<1>(k));
+    k = max(k, partner<2>(k));
+    k = max(k, partner<3>(k));
+    k = max(k, partner<4>(k));
+    k = max((uint32_t)__builtin_amdgcn_readlane((int)k, 0), (uint32_t)__builtin_amdgcn_readlane((int)k, 32));
+    return __uint_as_float(k);
+}
+
+// min over the wave of a non-negative float (+inf allowed)
+__device__ __forceinline__ float wave_min_nonneg(float x) {
+    uint32_t k = __float_as_uint(x);
+    k = min(k, partner<0>(k));
+    k = min(k, partner<1>(k));
+    k = min(k, partner<2>(k));
+    k = min(k, partner<3>(k));
+    k = min(k, partner<4>(k));
+    k = min((uint32_t)__builtin_amdgcn_readlane((int)k, 0), (uint32_t)__builtin_amdgcn_readlane((int)k, 32));
+    return __uint_as_float(k);
+}
+
 template <class C>
-__device__ __forceinline__ void a1_query(const float (&creg)[C::SL][C::D], const float* __restrict__ qv,
-                                         WaveRecT<C::SL>& rec, int vwave, int lane, uint32_t dmask) {
+__device__ __forceinline__ void a1_query(const float (&creg)[C::SL][C::DR], const float* __restrict__ qv,
+                                         WaveRecT<C::SL>& rec, int vwave, int lane, uint32_t dmask,
+                                         const float* __restrict__ trow = nullptr, int p0 = 0, float tw = 0.0f) {
     float dv[C::SL];
-    a1_dist<C::D, C::SL>(creg, qv, dv);
+    a1_dist<C::DR, C::SL>(creg, qv, dv);
+    if constexpr (C::SPLIT) {
+        // the reference's sum continued over the tail features, for the leaves
+        // that can hold the wave minimum: every partial sum over the first DR
+        // features is <= the full one, and the full sum of the leaf at the
+        // partial minimum mh is <= U = (mh + TW)(1 + 2^-18); a leaf above U
+        // keeps its partial sum -- a lower bound, above the minimum, never tied
+        float ml = __builtin_inff();
+#pragma unroll
+        for (int s = 0; s < C::SL; ++s) ml = ((dmask >> s) & 1u) ? ml : fminf(ml, dv[s]);
+        const float U = fmul(fadd(wave_min_nonneg(ml), tw), 1.0f + 0x1p-18f);
+#pragma unroll
+        for (int s = 0; s < C::SL; ++s)
+            if (!((dmask >> s) & 1u) && dv[s] <= U) {
+                const float* tr = trow + (int64_t)(p0 + s) * C::TL;
+                float a = dv[s];
+#pragma unroll
+                for (int d = 0; d < C::TL; ++d) {
+                    const float t = fsub(qv[C::DR + d], tr[d]);
+                    a = fadd(a, fmul(t, t));
+                }
+                dv[s] = a;
+            }
+    }
 #pragma unroll
     for (int s = 0; s < C::SL; ++s) dv[s] = ((dmask >> s) & 1u) ? __builtin_inff() : dv[s];  // padding leaves
     a1_reduce<C>(dv, rec, vwave, lane);
@@ -568,18 +629,6 @@ __device__ __forceinline__ float norm2_x(const float* __restrict__ v) {  // |v|^
 #pragma unroll
     for (int d = 0; d < D; ++d) n = __builtin_fmaf(v[d], v[d], n);
     return n;
-}
-
-// max over the wave of a non-negative float (bit order = value order)
-__device__ __forceinline__ float wave_max_nonneg(float x) {
-    uint32_t k = __float_as_uint(x);
-    k = max(k, partner<0>(k));
-    k = max(k, partner<1>(k));
-    k = max(k, partner<2>(k));
-    k = max(k, partner<3>(k));
-    k = max(k, partner<4>(k));
-    k = max((uint32_t)__builtin_amdgcn_readlane((int)k, 0), (uint32_t)__builtin_amdgcn_readlane((int)k, 32));
-    return __uint_as_float(k);
 }
 
 __device__ __forceinline__ float fsum16(float v) {  // sum over each aligned 16-lane row, uniform result
@@ -998,8 +1047,8 @@ __device__ __forceinline__ void dfs_parallel(Scan2Shared<C>& sh, int tid, int la
 
 // fold published log entries into the owners' registers
 template <class C>
-__device__ __forceinline__ void refresh(Scan2Shared<C>& sh, float (&creg)[C::SL][C::D], float (&cn)[C::SL],
-                                        float& cnmax, int vwave, int lane) {
+__device__ __forceinline__ void refresh(Scan2Shared<C>& sh, float (&creg)[C::SL][C::DR], float (&cn)[C::SL],
+                                        float& cnmax, int vwave, int lane, float* __restrict__ trow = nullptr) {
     constexpr int SL = C::SL, LS = C::LS, D = C::D;
     const int pp = sh.pub_pos[lane];
     uint64_t m = __ballot(pp >= 0 && (pp >> (6 + LS)) == vwave);
@@ -1021,12 +1070,16 @@ __device__ __forceinline__ void refresh(Scan2Shared<C>& sh, float (&creg)[C::SL]
         for (int s = 0; s < SL; ++s) {
             if (s == slot) {
 #pragma unroll
-                for (int d = 0; d < D; ++d) {
+                for (int d = 0; d < C::DR; ++d) {
                     const float v = sh.lg_c[e][d];
                     creg[s][d] = lane == owner ? v : creg[s][d];
                 }
                 cn[s] = lane == owner ? nv : cn[s];
             }
+        }
+        if constexpr (C::SPLIT) {  // the owner's tail row (only the owner lane ever reads it)
+            if (lane == owner)
+                for (int d = C::DR; d < D; ++d) trow[(int64_t)p * C::TL + (d - C::DR)] = sh.lg_c[e][d];
         }
     }
     if (any && lane == 0) sh.cnmax[vwave] = cnmax;
@@ -1037,8 +1090,9 @@ __device__ __forceinline__ void refresh(Scan2Shared<C>& sh, float (&creg)[C::SL]
 // minimum of the A1 records, as in A2) -- over this workgroup's waves only --
 // into recs[j].o
 template <class C>
-__device__ __forceinline__ void write_cstar(Scan2Shared<C>& sh, const float (&creg)[C::SL][C::D], QRecT<C::D>* recs,
-                                            uint64_t qmask, int col0, int wave, int lane, int wg) {
+__device__ __forceinline__ void write_cstar(Scan2Shared<C>& sh, const float (&creg)[C::SL][C::DR], QRecT<C::D>* recs,
+                                            uint64_t qmask, int col0, int wave, int lane, int wg,
+                                            const float* __restrict__ trow = nullptr) {
     constexpr int SL = C::SL, D = C::D, NWL = C::NWL;
     uint64_t won;
     {
@@ -1067,7 +1121,11 @@ __device__ __forceinline__ void write_cstar(Scan2Shared<C>& sh, const float (&cr
         for (int s = 0; s < SL; ++s)
             if (s == slot && lane == owner) {
 #pragma unroll
-                for (int d = 0; d < D; ++d) dst[d] = creg[s][d];
+                for (int d = 0; d < C::DR; ++d) dst[d] = creg[s][d];
+                if constexpr (C::SPLIT) {
+                    const float* tr = trow + (int64_t)(((wg * NWL + wave) * 64 + owner) * SL + s) * C::TL;
+                    for (int d = C::DR; d < D; ++d) dst[d] = tr[d - C::DR];
+                }
             }
     }
 }
@@ -1174,7 +1232,8 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                                                            const float* __restrict__ Xall, float* __restrict__ Call,
                                                            int* __restrict__ i_scratch,
                                                            const float* __restrict__ rate_tab, double tol,
-                                                           int max_passes, uint64_t* __restrict__ xbuf, int opts) {
+                                                           int max_passes, uint64_t* __restrict__ xbuf, int opts,
+                                                           float* __restrict__ Tall) {
     constexpr int D = C::D, K = C::K, SL = C::SL, LS = C::LS, NWL = C::NWL, KB = C::KB, NWG = C::NWG;
     constexpr int kErrWave = NWL > 1 ? 1 : 0;  // residual + cluster ids (wave 0 keeps the log)
     constexpr bool PRUNE = NWG == 1;           // A1 pruning by wave boxes (one-CU frames)
@@ -1211,6 +1270,8 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     int* clusters = uniform_ptr(i_scratch + frp->n_off);
     int* prev_cnt = uniform_ptr(i_scratch + frp->k_off);  // cnts[not Odd(iter)] by centroid id
     int* cnta = uniform_ptr(i_scratch + frp->ka_off);     // cnts[Odd(iter)] by kd-leaf position
+    // split layout: the tail features of kd-leaf position p at trow + p * TL
+    float* trow = C::SPLIT ? uniform_ptr(Tall + frp->t_off) : nullptr;
     XPort xp{nullptr, nullptr, 0};
     if constexpr (NWG == 2) {
         xp.mine = xbuf + ((size_t)fi * 2 + wg) * 2 * kXCap;
@@ -1261,27 +1322,44 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         if (tid == 0 && wg0) frp->tree_exact += 1;
     }
 
-    float creg[SL][D];
-    float cn[SL];  // |c|^2 per register leaf (A1 bounds); +inf for padding leaves
+    float creg[SL][C::DR];
+    float cn[SL];  // |c|^2 (over the register features) per register leaf (A1 bounds); +inf for padding leaves
     const int p0 = (vwave * 64 + lane) * SL;
     bool nan_here = false;
     uint32_t dmask = 0;  // slots that hold no centroid (past K, or padding leaves)
+    constexpr int TLA = C::TL > 0 ? C::TL : 1;
+    float tlo[TLA], thi[TLA];  // split layout: this lane's tail box
+#pragma unroll
+    for (int d = 0; d < TLA; ++d) {
+        tlo[d] = __builtin_inff();
+        thi[d] = -__builtin_inff();
+    }
 #pragma unroll
     for (int s = 0; s < SL; ++s) {
         const int p = p0 + s;
         const int id = p < K ? (int)sh.t.pidx[p] : 0xFFFF;
         if (id != 0xFFFF) {
 #pragma unroll
-            for (int d = 0; d < D; ++d) {
+            for (int d = 0; d < C::DR; ++d) {
                 creg[s][d] = C_[(int64_t)id * D + d];
                 nan_here |= creg[s][d] != creg[s][d];
+            }
+            if constexpr (C::SPLIT) {  // the tail features go to the lane's rows of the tail array
+#pragma unroll
+                for (int d = 0; d < C::TL; ++d) {
+                    const float v = C_[(int64_t)id * D + C::DR + d];
+                    trow[(int64_t)p * C::TL + d] = v;
+                    nan_here |= v != v;
+                    tlo[d] = fminf(tlo[d], v);
+                    thi[d] = fmaxf(thi[d], v);
+                }
             }
         } else {
             dmask |= 1u << s;
 #pragma unroll
-            for (int d = 0; d < D; ++d) creg[s][d] = 0.0f;
+            for (int d = 0; d < C::DR; ++d) creg[s][d] = 0.0f;
         }
-        cn[s] = id != 0xFFFF ? norm2_x<D>(creg[s]) : __builtin_inff();
+        cn[s] = id != 0xFFFF ? norm2_x<C::DR>(creg[s]) : __builtin_inff();
     }
     if constexpr (PRUNE) {  // the half-dimension bound's inputs: H-norm maxima, tail box of the centroids
         float mh = 0.0f;
@@ -1292,12 +1370,17 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
 #pragma unroll
         for (int d = C::H; d < D; ++d) {
             float lo = __builtin_inff(), hi = -__builtin_inff();
+            if constexpr (C::SPLIT) {
+                lo = tlo[d - C::H];
+                hi = thi[d - C::H];
+            } else {
 #pragma unroll
-            for (int s = 0; s < SL; ++s)
-                if (!((dmask >> s) & 1u)) {
-                    lo = fminf(lo, creg[s][d]);
-                    hi = fmaxf(hi, creg[s][d]);
-                }
+                for (int s = 0; s < SL; ++s)
+                    if (!((dmask >> s) & 1u)) {
+                        lo = fminf(lo, creg[s][d < C::DR ? d : 0]);
+                        hi = fmaxf(hi, creg[s][d < C::DR ? d : 0]);
+                    }
+            }
             const int klo = wave_min_i(ordkey(__float_as_uint(lo)));
             const int khi = wave_max_i(ordkey(__float_as_uint(hi)));
             if (lane == 0) {
@@ -1350,7 +1433,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     // and the pass's centroids (tail features), with an ulp-scale slack per
     // feature for the rounding of the online moves
     bool half = false;
-    float twh = 0.0f, te = 0.0f;
+    float twh = 0.0f, te = 0.0f, tw_pass = 0.0f;
     if constexpr (PRUNE) {
         float tw = 0.0f, tn = 0.0f;
 #pragma unroll
@@ -1367,6 +1450,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             tn = fadd(tn, fmul(mag, mag));
         }
         tw = fmul(tw, 1.0f + 0x1p-10f);
+        tw_pass = tw;
         float mh = 0.0f;
 #pragma unroll
         for (int w = 0; w < C::NWV; ++w) mh = fmaxf(mh, sh.cnmax_h[w]);
@@ -1375,8 +1459,9 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         // worth it while the tail slack is a small part of eps's norm scale
         half = !(tw != tw) && te <= fmul(fmul(mh, C::EPSF), 0.25f) && !uniform_int(sh.any_nan) && !no_half;
     }
-    if (uniform_int(sh.any_nan)) {
-        // NaN centroids (yakmo 0/0 means) make ANN's early exits order dependent:
+    if (uniform_int(sh.any_nan) || (C::SPLIT && !half)) {
+        // NaN centroids (yakmo 0/0 means) make ANN's early exits order dependent;
+        // the split layout has no full-dimension bound (a tail too wide for eps):
         // this pass runs in the generic kernel (gsc_kernels.hip)
         if (tid == 0 && wg0) {
             frp->generic = 1;
@@ -1436,9 +1521,9 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 const int j1 = m ? __ffsll((long long)m) - 1 : j0;
                 if (m) m &= m - 1;
                 float dv0[SL], dv1[SL];
-                if (half)
-                    a1_dist_x2<C::H, D, SL>(creg, cn, sh.qm[cur_buf][j0], sh.qm[cur_buf][j1], dv0, dv1);
-                else
+                if (C::SPLIT || half)
+                    a1_dist_x2<C::H, C::DR, SL>(creg, cn, sh.qm[cur_buf][j0], sh.qm[cur_buf][j1], dv0, dv1);
+                else if constexpr (!C::SPLIT)
                     a1_dist_x2<D, D, SL>(creg, cn, sh.qm[cur_buf][j0], sh.qm[cur_buf][j1], dv0, dv1);
                 a1_reduce2<C>(dv0, dv1, sh.wrec[vwave][j0], sh.wrec[vwave][j1], vwave, lane);
             }
@@ -1497,7 +1582,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         if (cur_n > 0) {
             // c*'s snapshot coordinates (and exact distance), written by the wave that owns c*
             if constexpr (NWG == 1)
-                write_cstar<C>(sh, creg, sh.qrec[cur_buf], (1ull << cur_n) - 1ull, 0, wave, lane, 0);
+                write_cstar<C>(sh, creg, sh.qrec[cur_buf], (1ull << cur_n) - 1ull, 0, wave, lane, 0, trow);
             STAMP(8)
 #pragma unroll 1
             for (int j0 = wave * 4; j0 < cur_n; j0 += 4 * NWL)
@@ -1524,7 +1609,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                         const float lb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbp), jj));
                         if (lane == 0) sh.wrec[vwave][jj].minbits = __float_as_uint(lb);
                     } else {
-                        a1_query<C>(creg, sh.q[cur_buf][jj], sh.wrec[vwave][jj], vwave, lane, dmask);
+                        a1_query<C>(creg, sh.q[cur_buf][jj], sh.wrec[vwave][jj], vwave, lane, dmask, trow, p0, tw_pass);
                     }
                 }
                 lds_barrier();
@@ -1535,7 +1620,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                     lds_barrier();
                     fill_winner_coords<C>(sh, sh.qrec[cur_buf], nfx, sh.fxl, 0, tid, wg);
                 } else {
-                    write_cstar<C>(sh, creg, sh.qrec[cur_buf], fx, 0, wave, lane, 0);
+                    write_cstar<C>(sh, creg, sh.qrec[cur_buf], fx, 0, wave, lane, 0, trow);
                 }
 #pragma unroll 1
                 for (int j0 = wave * 4; j0 < nfx; j0 += 4 * NWL)
@@ -1655,12 +1740,12 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         lds_barrier();
         STAMP(4)
         // ---- part 4: fold the log into the registers
-        refresh<C>(sh, creg, cn, cnmax, vwave, lane);
+        refresh<C>(sh, creg, cn, cnmax, vwave, lane, trow);
         if (solo_j >= 0) {
             // the failed query on the live centroids: fresh distances and
             // certificate; exact DFS if the certificate still fails
             ++restarts;
-            a1_query<C>(creg, sh.qslow, sh.wrec[vwave][KB], vwave, lane, dmask);
+            a1_query<C>(creg, sh.qslow, sh.wrec[vwave][KB], vwave, lane, dmask, trow, p0, tw_pass);
             lds_barrier();
             if constexpr (NWG == 2) {
                 write_cstar<C>(sh, creg, &sh.qsolo, 1ull, KB, wave, lane, wg);
@@ -1685,12 +1770,23 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
 #pragma unroll
                 for (int s = 0; s < SL; ++s) dv[s] = 0.0f;
 #pragma unroll
-                for (int d = 0; d < D; ++d) {
+                for (int d = 0; d < C::DR; ++d) {
                     const float qd = sh.qslow[d];
 #pragma unroll
                     for (int s = 0; s < SL; ++s) {
                         const float t = fsub(qd, creg[s][d]);
                         dv[s] = fadd(dv[s], fmul(t, t));
+                    }
+                }
+                if constexpr (C::SPLIT) {  // every leaf's full live distance: the tail rows (rare path)
+#pragma unroll
+                    for (int s = 0; s < SL; ++s) {
+                        const float* tr = trow + (int64_t)(p0 + s) * C::TL;
+                        if (!((dmask >> s) & 1u))
+                            for (int d = 0; d < C::TL; ++d) {
+                                const float t = fsub(sh.qslow[C::DR + d], tr[d]);
+                                dv[s] = fadd(dv[s], fmul(t, t));
+                            }
                     }
                 }
 #pragma unroll
@@ -1719,7 +1815,9 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             for (int s = 0; s < SL; ++s)
                 if (s == slot && tid == owner_t) {
 #pragma unroll
-                    for (int d = 0; d < D; ++d) sh.solo_c[d] = creg[s][d];
+                    for (int d = 0; d < C::DR; ++d) sh.solo_c[d] = creg[s][d];
+                    if constexpr (C::SPLIT)
+                        for (int d = C::DR; d < D; ++d) sh.solo_c[d] = trow[(int64_t)bpos * C::TL + (d - C::DR)];
                 }
             if constexpr (NWG == 2) {
                 lds_barrier();
@@ -1762,7 +1860,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 sh.pub_pos[lane] = lane == e ? bpos : -1;
             }
             lds_barrier();
-            refresh<C>(sh, creg, cn, cnmax, vwave, lane);
+            refresh<C>(sh, creg, cn, cnmax, vwave, lane, trow);
         }
         STAMP(5)
         if (nvq == 0 && cur_n == 0) {
@@ -1785,7 +1883,9 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         if (!((dmask >> s) & 1u)) {
             const int id = sh.t.pidx[p];
 #pragma unroll
-            for (int d = 0; d < D; ++d) C_[(int64_t)id * D + d] = creg[s][d];
+            for (int d = 0; d < C::DR; ++d) C_[(int64_t)id * D + d] = creg[s][d];
+            if constexpr (C::SPLIT)
+                for (int d = C::DR; d < D; ++d) C_[(int64_t)id * D + d] = trow[(int64_t)p * C::TL + (d - C::DR)];
         }
     }
     if (wg0)
@@ -1841,7 +1941,7 @@ using namespace gsc;
 template <class C>
 static hipError_t launch_scan(ReduceFrame* frames, int nframes, const float* X, float* Cc, int* is,
                               const float* rate_tab, double tol, int max_passes, uint64_t* xbuf, int opts,
-                              hipStream_t st) {
+                              float* tails, hipStream_t st) {
     const size_t shm = sizeof(Scan2Shared<C>);
     static_assert(sizeof(Scan2Shared<C>) <= 160 * 1024, "LDS budget (160 KB per CU)");
     hipError_t e = hipFuncSetAttribute((const void*)scan_batch_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1849,7 +1949,7 @@ static hipError_t launch_scan(ReduceFrame* frames, int nframes, const float* X, 
     if (e != hipSuccess) return e;
     if constexpr (C::NWG == 1) {
         hipLaunchKernelGGL(scan_batch_kernel<C>, dim3(nframes), dim3(C::NT), shm, st, frames, nframes, X, Cc, is,
-                           rate_tab, tol, max_passes, xbuf, opts);
+                           rate_tab, tol, max_passes, xbuf, opts, tails);
         return hipGetLastError();
     } else {
         // both workgroups of a frame must be resident together: a cooperative
@@ -1859,7 +1959,7 @@ static hipError_t launch_scan(ReduceFrame* frames, int nframes, const float* X, 
         if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
         int pairs = std::min(nframes, std::max(1, cus / 2));
         if (pairs >= 8) pairs -= pairs % 8;  // whole groups of 16 workgroups: pair members share an XCD
-        void* args[] = {&frames, &nframes, &X, &Cc, &is, &rate_tab, &tol, &max_passes, &xbuf, &opts};
+        void* args[] = {&frames, &nframes, &X, &Cc, &is, &rate_tab, &tol, &max_passes, &xbuf, &opts, &tails};
         return hipLaunchCooperativeKernel((const void*)scan_batch_kernel<C>, dim3(2 * pairs), dim3(C::NT), args, shm,
                                           st);
     }
@@ -1874,18 +1974,26 @@ static hipError_t launch_scan(ReduceFrame* frames, int nframes, const float* X, 
 // not cover.
 extern "C" hipError_t gsc_launch_scan_batch(int D, int logk, ReduceFrame* frames, int nframes, const float* X,
                                             float* Cc, int* is, const float* rate_tab, double tol, int max_passes,
-                                            uint64_t* xbuf, int opts, hipStream_t st) {
+                                            uint64_t* xbuf, int opts, float* tails, hipStream_t st) {
 #define SB(DV, LK, SLV, NG)                                                                                    \
     if (D == DV && logk == LK)                                                                                 \
         return launch_scan<ScanCfg<DV, LK, SLV, NG>>(frames, nframes, X, Cc, is, rate_tab, tol, max_passes, xbuf, \
-                                                     opts, st);
+                                                     opts, tails, st);
     // K below 4096: four leaves per lane, so a frame gets twice the waves
     // (K = 512: two instead of one); the per-search work there is latency
     SB(8, 8, 4, 1) SB(8, 9, 4, 1) SB(8, 10, 4, 1) SB(8, 11, 4, 1) SB(8, 12, 8, 1)
     SB(16, 8, 4, 1) SB(16, 9, 4, 1) SB(16, 10, 4, 1) SB(16, 11, 4, 1) SB(16, 12, 8, 1)
-    SB(32, 8, 4, 1) SB(32, 9, 4, 1) SB(32, 10, 4, 1) SB(32, 11, 4, 1) SB(32, 12, 4, 2)
+    SB(32, 8, 4, 1) SB(32, 9, 4, 1) SB(32, 10, 4, 1) SB(32, 11, 4, 1)
+    // D = 32, K = 4096: one CU per frame, the DCT half of every centroid in
+    // VGPRs and the cepstrum half in the frame's tail array (split layout)
+    if (D == 32 && logk == 12)
+        return launch_scan<ScanCfg<32, 12, 8, 1, 16>>(frames, nframes, X, Cc, is, rate_tab, tol, max_passes, xbuf,
+                                                      opts, tails, st);
 #undef SB
     return hipErrorInvalidValue;
 }
 
 extern "C" size_t gsc_scan_xbuf_granules_per_frame(void) { return 2 * 2 * (size_t)kXCap; }
+
+// floats of the split layout's tail array per frame (0: the shape keeps every feature in VGPRs)
+extern "C" size_t gsc_scan_tail_floats_per_frame(int D, int logk) { return D == 32 && logk == 12 ? 4096 * 16 : 0; }

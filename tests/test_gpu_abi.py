@@ -152,16 +152,17 @@ def test_knnfit_replay_matches_oracle(oracle, frame):
     np.testing.assert_array_equal(got, frame["knn_best"][:1500])
 
 
-@pytest.mark.parametrize("k", [1, 7, 64])
-def test_search_exports_stale_tree(oracle, k):
+@pytest.mark.parametrize("k,n", [(1, 300), (7, 300), (64, 300), (7, 3000)])
+def test_search_exports_stale_tree(oracle, k, n):
     """ann_kdtree_search_multi / pri_search_multi / pri_search vs ANN's
-    restatement, on a tree whose points then move (every search reads live rows)."""
+    restatement, on a tree whose points then move (every search reads live rows).
+    n = 3000 also runs the build's wave-per-node levels (segments >= 512)."""
     import soundchunks_amd as sc
 
     lib = sc.load()
     ora = _ora_tree_api(oracle.load())
-    rng = np.random.default_rng(7 + k)
-    pts = np.round(rng.normal(size=(300, 8)) * 8).astype(np.float32) / 8  # coarse grid: exact ties
+    rng = np.random.default_rng(7 + k + n)
+    pts = np.round(rng.normal(size=(n, 8)) * 8).astype(np.float32) / 8  # coarse grid: exact ties
     pa = _rows(pts)
     t = lib.ann_kdtree_create(pa, pts.shape[0], 8, 1, 0)
     o = ora.ora_kdtree_create(pa, pts.shape[0], 8, 1)

@@ -68,7 +68,8 @@ def c3_trace(oracle):
 
 @pytest.mark.parametrize("passes", [1, 3])
 def test_scan_k4096_d32_first_passes(oracle, c3_trace, passes):
-    """D = 32 (ChunkSize 16): each frame on two CUs exchanging A1 records."""
+    """D = 32 (ChunkSize 16) at K = 4096: one CU per frame in the split layout
+    (DCT half of each centroid in VGPRs, cepstrum half in the frame's tail array)."""
     import soundchunks_amd as sc
 
     os.environ["GSC_SCAN_MAX_PASSES"] = str(passes)
@@ -91,9 +92,10 @@ def test_scan_k4096_d32_full(c3_trace):
     np.testing.assert_array_equal(_bits(gc), _bits(c3_trace["scan"]))
 
 
-@pytest.mark.parametrize("k", [256, 2048])
+@pytest.mark.parametrize("k", [256, 2048, 3000])
 def test_scan_d32_one_cu(oracle, c3_trace, k):
-    """D = 32 with K <= 2048 fits one CU (4 leaves per lane)."""
+    """D = 32: K <= 2048 keeps every feature in VGPRs (4 leaves per lane); K = 3000
+    runs the split layout over the padded 4096-leaf tree."""
     import soundchunks_amd as sc
 
     x = c3_trace["dataset"][:6000]
