@@ -795,11 +795,22 @@ int Encoder::device_recon(int b, const std::vector<FrameState>& frames, ReconOut
     return 0;
 }
 
+// test hook (tests/test_gpu_encoder.py): GSC_TEST_FAIL_POST set makes ONE
+// post_group call of the process fail, while the scan may still be running
+static bool inject_post_failure() {
+    static std::atomic<int> used{0};
+    return std::getenv("GSC_TEST_FAIL_POST") != nullptr && used.exchange(1) == 0;
+}
+
 int Encoder::post_group(std::vector<FrameState>& frames, const std::vector<int>& ids,
                         const std::vector<char>& reduced, PostCtx& c, std::string* err) {
     const int cs = opt_.chunk_size, bd = opt_.chunk_bit_depth, obd = (1 << (bd - 1)) - 1;
     const int g = int(ids.size());
     if (g == 0) return 0;
+    if (inject_post_failure()) {
+        *err = "injected post_group failure (GSC_TEST_FAIL_POST)";
+        return -1;
+    }
     auto chk = [&](hipError_t r, const char* what) {
         if (r == hipSuccess) return true;
         *err = std::string("KNNFit/pack pipeline: ") + what + ": " + hipGetErrorString(r);

@@ -1094,7 +1094,11 @@ __device__ __forceinline__ void write_cstar(Scan2Shared<C>& sh, const float (&cr
                                             uint64_t qmask, int col0, int wave, int lane, int wg,
                                             const float* __restrict__ trow = nullptr) {
     constexpr int SL = C::SL, D = C::D, NWL = C::NWL;
+    // lane = query: the winning wave (first at the minimum) and, for this
+    // wave's wins, the owner lane and slot from its record -- all queries at
+    // once, so the copy loop below has no LDS round trip per query
     uint64_t won;
+    int ol = 0;  // owner lane << 8 | slot
     {
         const bool act = (qmask >> lane) & 1ull;
         const int jq = act ? lane : 0;
@@ -1109,13 +1113,18 @@ __device__ __forceinline__ void write_cstar(Scan2Shared<C>& sh, const float (&cr
             }
         }
         won = __ballot(act && W == wave);
+        if (act && W == wave) {
+            const WaveRecT<SL>& r = sh.wrec[wg * NWL + wave][col0 + jq];
+            bool tie2;
+            const int slot = rec_slot<SL>(r, &tie2);
+            ol = ((r.lanebits & 255) << 8) | slot;
+        }
     }
     while (won) {
         const int jj = __ffsll((long long)won) - 1;
         won &= won - 1;
-        const WaveRecT<SL>& r = sh.wrec[wg * NWL + wave][col0 + jj];
-        bool tie2;
-        const int owner = r.lanebits & 255, slot = rec_slot<SL>(r, &tie2);
+        const int o = __builtin_amdgcn_readlane(ol, jj);
+        const int owner = o >> 8, slot = o & 255;
         float* dst = recs[jj].o;
 #pragma unroll
         for (int s = 0; s < SL; ++s)

@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread \
-  -k "d32 or c3 or cs16 or corpus_as_one_batch or two_rank_hip or stale_tree or overflow or knnfit" > gpurun_out/r03_f_test.log 2>&1
+  -k "d32 or c3 or cs16 or corpus_as_one_batch or two_rank_hip or stale_tree or overflow or knnfit or drains" > gpurun_out/r03_f_test.log 2>&1
 rc=$?; tail -3 gpurun_out/r03_f_test.log; [ $rc -ne 0 ] && exit $rc
 GSC_HOST_TIMING=1 timeout -k 10 300 python -u bench.py --config c3 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/r03_f_c3.log 2>&1 || exit 4
 grep -E "host timing|passes histogram" gpurun_out/r03_f_c3.log | tail -2; tail -1 gpurun_out/r03_f_c3.log | cut -c1-400
