@@ -48,6 +48,8 @@ struct ScanShared {
     int wok[8];
     int slow_pos;
     float slow_key;
+    int any_nan;                // some centroid of this pass is NaN (yakmo 0/0 means)
+    uint8_t nanpos[kMaxK];      // kd-leaf position holds a NaN centroid (fixed for the pass)
 };
 
 struct MinRec {
@@ -112,6 +114,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
     int* clusters = uniform_ptr(i_scratch + frp->n_off);
     int* prev_cnt = uniform_ptr(i_scratch + frp->k_off);  // cnts[not Odd(iter)] by centroid id
     float* box0 = uniform_ptr(f_scratch + frp->n_off * 3);  // root box per query (yakmo scratch reused)
+    int* first = reinterpret_cast<int*>(box0 + N);            // first leaf of ANN's descent per query
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nthreads = blockDim.x, nwaves = nthreads >> 6;
     const bool pow2 = (K & (K - 1)) == 0;
@@ -119,6 +122,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
 
     if (pass == 0)
         for (int k = tid; k < K; k += nthreads) prev_cnt[k] = 1;  // CCntStart (encoder.lpr:717-721)
+    if (tid == 0) sh.any_nan = 0;
     __syncthreads();
     build_tree<D>(sh.t, sh.dist, C, K);
     // annBoxDistance(q, bnd_lo, bnd_hi) for every query of this pass
@@ -137,6 +141,21 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
             }
         }
         box0[i] = box;
+        // the leaf ANN's DFS reaches first: near children only (annkSearch never
+        // prunes on the way down); the stale tree fixes it for the whole pass
+        int h = 0, s = 0, n = K;
+        while (n > 1) {
+            const int half = n >> 1;
+            if (fsub(qp[sh.t.cd[h]], sh.t.cv[h]) < 0.0f) {
+                h = 2 * h + 1;
+                n = half;
+            } else {
+                h = 2 * h + 2;
+                s += half;
+                n -= half;
+            }
+        }
+        first[i] = s;
     }
 
     float creg[kScanSlots][D];
@@ -150,6 +169,13 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
             for (int d = 0; d < D; ++d) creg[s][d] = C[(int64_t)id * D + d];
             sh.rate[p] = rate_tab[prev_cnt[id]];  // Single(1/sqrt(cnts[not Odd(iter)]))
             sh.cnta[p] = 1;
+            // a centroid is NaN for the whole pass or for none of it: a NaN row
+            // stays NaN under c + (x - c) * rate, a finite one stays finite
+            bool nn = false;
+#pragma unroll
+            for (int d = 0; d < D; ++d) nn |= creg[s][d] != creg[s][d];
+            sh.nanpos[p] = nn ? 1 : 0;
+            if (nn) sh.any_nan = 1;
         } else {
 #pragma unroll
             for (int d = 0; d < D; ++d) creg[s][d] = 0.0f;
@@ -223,7 +249,13 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
             o.pos = sh.wpos[w];
             g = min_combine(g, o);
         }
-        bool fast = (g.cnt == 1) && (g.v <= FLT_MAX);
+        // NaN centroids: a NaN leaf reached first becomes ANN's answer (its
+        // key NaN fails every later box' < key test, so the DFS ends there);
+        // after a real first leaf every NaN leaf is inert (key > NaN is false),
+        // so the certificate below may treat NaN distances as +inf
+        const int fl = uniform_int(sh.any_nan) ? uniform_int(first[i]) : -1;
+        const bool nanfirst = fl >= 0 && sh.nanpos[fl] != 0;
+        bool fast = !nanfirst && (g.cnt == 1) && (g.v <= FLT_MAX);
         const int pstar = g.pos;
         if (fast) {
             // lane l < maxdepth evaluates the split node at depth l on c*'s path
@@ -308,7 +340,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
                     if ((farmask >> lv0) & 1ull) {
 #pragma unroll
                         for (int s2 = 0; s2 < kScanSlots; ++s2)
-                            if (p0 + s2 < K && !(dv[s2] > thr0)) ok = false;
+                            if (p0 + s2 < K && dv[s2] <= thr0) ok = false;
                     }
                 } else {
 #pragma unroll
@@ -316,7 +348,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
                         const int p = p0 + s2;
                         if (p >= K || p == pstar) continue;
                         const int lv = lca_depth(p, pstar, K, log2K, pow2);
-                        if (((farmask >> lv) & 1ull) && !(dv[s2] > sh.wB[wave][lv])) ok = false;
+                        if (((farmask >> lv) & 1ull) && dv[s2] <= sh.wB[wave][lv]) ok = false;
                     }
                 }
             }
@@ -328,7 +360,10 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
         for (int w = 0; w < nwaves; ++w) allok = allok && (sh.wok[w] != 0);
         int bpos;
         float bkey;
-        if (allok) {
+        if (nanfirst) {
+            bpos = fl;
+            bkey = __builtin_nanf("");
+        } else if (allok) {
             bpos = pstar;
             bkey = g.v;
         } else {

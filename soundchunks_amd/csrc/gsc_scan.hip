@@ -149,7 +149,7 @@ struct QRecT {        // A2 output per query
     float m2;         // snapshot minimum over every other leaf
     float rate;       // Single(1/sqrt(previous-pass count of c*))
     uint32_t farmask; // far steps on c*'s root path, bit = depth
-    int pad_;
+    int pad_;         // 1: NaN-first query (ANN answers the NaN leaf its descent reaches)
     float B[16];      // suffix max of box' over far steps (certificate thresholds)
     float o[D];       // c*'s snapshot coordinates
 };
@@ -203,6 +203,8 @@ struct Scan2Shared {
     int slow_pos;
     float slow_key;
     int any_nan;
+    int nan_rows;          // the pass has NaN centroids (yakmo 0/0 means): see nan_first below
+    uint32_t nanid[kMaxK / 32];  // centroid id -> NaN row (fixed for the whole pass)
     int pass_done;         // end of pass: the frame converged (or hands the next pass over)
     uint32_t wkey[2][C::NWL];  // parallel exact DFS: per-wave next-improvement keys
     alignas(16) float a2s[C::NWL][C::D > 16 ? 2 : 1][64];  // A2 scratch per wave: box terms by dimension
@@ -644,7 +646,7 @@ __device__ __forceinline__ float fsum16(float v) {  // sum over each aligned 16-
 template <class C, bool APPROX>
 __device__ __forceinline__ void a2_group(Scan2Shared<C>& sh, int j0, int nq, const float (*qrows)[C::QD],
                                          QRecT<C::D>* recs, int wcol0, const int* jlist, int lane,
-                                         bool half = false, float twh = 0.0f, float te = 0.0f
+                                         bool half = false, float twh = 0.0f, float te = 0.0f, bool nanpass = false
 #ifdef GSC_STAMPS
                                          , uint64_t* acc = nullptr, uint64_t* tl = nullptr
 #endif
@@ -787,17 +789,36 @@ __device__ __forceinline__ void a2_group(Scan2Shared<C>& sh, int j0, int nq, con
     if (far && inc != inc) ok = false;  // a NaN box' is never visited (fmaxf would drop it from B)
     const bool gok = ((__ballot(!ok) >> gbase) & 0xFFFFull) == 0;
     const bool valid = unique && __uint_as_float(gmin) <= FLT_MAX && gok;
+    // NaN centroids (their leaves carry +inf in every distance here): ANN's DFS
+    // reaches first the leaf of the near-child descent; a NaN leaf there becomes
+    // the answer with key NaN (every later box' < NaN test fails) -- otherwise
+    // NaN leaves are inert (key > NaN is false), which the +inf distances model.
+    // The descent equals c*'s root path when no step of it is far.
+    int nanf = -1;
+    if (APPROX && nanpass && qa && l == 0 && farmask != 0) {
+        int h = 0, pos = 0;
+#pragma unroll 1
+        for (int lv = 0; lv < LOGK; ++lv) {
+            const int bit = fsub(q[sh.t.cd[h]], sh.t.cv[h]) < 0.0f ? 0 : 1;
+            pos = 2 * pos + bit;
+            h = 2 * h + 1 + bit;
+        }
+        const int id = sh.t.pidx[pos];
+        if (id != 0xFFFF && ((sh.nanid[id >> 5] >> (id & 31)) & 1u)) nanf = pos;
+    }
     if (qa) {
         QRecT<D>& R = recs[jj];
         if (l < LOGK) R.B[l] = Bv;
         if (l == 0) {
-            R.valid = valid ? 1 : 0;
-            R.cstar = cstar;
-            R.id = sh.t.pidx[cstar];
-            R.g = __uint_as_float(gmin);  // exact mode only (the solo query); batch queries: vp_end
+            const int cs = nanf >= 0 ? nanf : cstar;
+            R.valid = (valid || nanf >= 0) ? 1 : 0;
+            R.cstar = cs;
+            R.id = sh.t.pidx[cs];
+            R.g = nanf >= 0 ? __builtin_nanf("") : __uint_as_float(gmin);  // exact mode only (the solo query); batch queries: vp_end
             R.m2 = m2lo;
-            R.rate = sh.rate[cstar];
+            R.rate = sh.rate[cs];
             R.farmask = farmask;
+            R.pad_ = nanf >= 0 ? 1 : 0;  // NaN-first query: no move, no check, residual NaN
         }
     }
     ASTAMP(15)
@@ -820,7 +841,8 @@ template <class C>
 __device__ __forceinline__ void vp_begin(Scan2Shared<C>& sh, int qb, int off, int pn, int a1, int lane, int& lg_pos,
                                          int lg_tag, VPState& st) {
     if (lg_pos >= 0 && lg_tag < a1) lg_pos = -1;  // committed before the batch's snapshot
-    st.cs = lane < pn ? sh.qrec[qb][off + lane].cstar : -2;
+    // a NaN-first query moves nothing: a key of its own, so it joins no chain and no log entry
+    st.cs = lane < pn ? (sh.qrec[qb][off + lane].pad_ ? -100 - lane : sh.qrec[qb][off + lane].cstar) : -2;
     sh.vpos[lane] = lg_pos;
     sh.vfrom[lane] = 0;
     if (lane < C::KB) sh.vcs[lane] = st.cs;
@@ -883,8 +905,9 @@ __device__ __forceinline__ void vp_end(Scan2Shared<C>& sh, int qb, int off, int 
             for (int d = 0; d < D; ++d) oc[d] = o[d];
             // exact live distance to c* (its snapshot coordinates when unmoved;
             // the A1 values of the batch are bounds only)
-            const float gpj = seqdist<D>(qv, oc);
-            const bool okc = R.valid != 0 && (pred < 0 || gpj < R.m2);
+            const bool nanq = R.pad_ != 0;
+            const float gpj = nanq ? __builtin_nanf("") : seqdist<D>(qv, oc);
+            const bool okc = nanq || (R.valid != 0 && (pred < 0 || gpj < R.m2));
             const float rate = R.rate;
 #pragma unroll
             for (int d = 0; d < D; ++d) sh.newc[j][d] = fadd(oc[d], fmul(fsub(qv[d], oc[d]), rate));
@@ -905,9 +928,9 @@ template <class C>
 __device__ __forceinline__ void v_check_q(Scan2Shared<C>& sh, int qb, int off, int pn, int wave, int lane) {
     constexpr int D = C::D, KB = C::KB, QPL = 64 / KB, LOGK = C::LOGK;
     const int j = lane % KB, grp = lane / KB;
-    const bool act = j < pn;
-    const int jr = act ? j : 0;
+    const int jr = j < pn ? j : 0;
     const QRecT<D>& R = sh.qrec[qb][off + jr];
+    const bool act = j < pn && R.pad_ == 0;  // a NaN-first answer holds whatever moved
     const int cs = R.cstar;
     const uint32_t fm = R.farmask;
     const float g = sh.gp[jr];
@@ -941,8 +964,10 @@ __device__ __forceinline__ void v_check_q(Scan2Shared<C>& sh, int qb, int off, i
 // along a path, so that is one test on its innermost far subtree (start rank
 // s*, box' bx*).  The next improvement is the lowest-ranked reached leaf with
 // d < b, found by one block min-reduction per improvement.  Live leaf
-// distances come from sh.dist.  No NaN distances reach this kernel (those
-// passes run the generic kernel), so leaf early exits cannot change a result.
+// distances come from sh.dist.  Passes with NaN centroids do not come here:
+// their trees can have cells whose bounds contradict the cut values (NaN cuts
+// upstream), so box' can shrink along a path (negative increments) and the
+// innermost-far-subtree test is not enough; they run scan_exact_dfs.
 template <class C>
 __device__ __forceinline__ void dfs_parallel(Scan2Shared<C>& sh, int tid, int lane, int wave, int& out_pos,
                                              float& out_key) {
@@ -1043,6 +1068,85 @@ __device__ __forceinline__ void dfs_parallel(Scan2Shared<C>& sh, int tid, int la
     }
     out_pos = bp;
     out_key = b;
+}
+
+// ANN's k = 1 search (annkSearch @0x1800124b0) over the stale tree with the
+// live distances in sh.dist, one lane, the recursion stack in LDS (dfs_inc,
+// free in passes that take this path): the NaN passes' exact DFS.  Their NaN
+// leaves carry +inf (inert: the query's descent reached a real leaf first), so
+// no leaf early exit changes a result; box' is tested at every far step, in
+// ANN's order, whatever its sign.  Same walk as scan_exact_dfs (gsc_tree.h),
+// kept in registers + LDS so the kernel's register block is not spilled
+// around a call.
+template <class C>
+__device__ __forceinline__ void dfs_exact_lds(Scan2Shared<C>& sh, int& out_pos, float& out_key) {
+    constexpr int D = C::D, K = C::K;
+    int* st_h = reinterpret_cast<int*>(sh.dfs_inc);
+    int* st_s = st_h + 16;
+    int* st_n = st_h + 32;
+    float* st_box = sh.dfs_inc + 48;
+    const float* q = sh.qslow;
+    float cur_box = 0.0f;
+    for (int d = 0; d < D; ++d) {  // annBoxDistance
+        const float qd = q[d];
+        if (qd < sh.t.bnd_lo[d]) {
+            const float t = fsub(sh.t.bnd_lo[d], qd);
+            cur_box = fadd(cur_box, fmul(t, t));
+        } else if (qd > sh.t.bnd_hi[d]) {
+            const float t = fsub(qd, sh.t.bnd_hi[d]);
+            cur_box = fadd(cur_box, fmul(t, t));
+        }
+    }
+    int sp = 0, best = -1, h = 0, s = 0, n = K;
+    float key = FLT_MAX;  // max_key of the empty list (ANN_DIST_INF)
+    for (;;) {
+        if (n == 1) {
+            const float dd = sh.dist[s];
+            if (!(dd > key) && (best < 0 || key > dd)) {  // ANNkd_leaf::ann_search + ANNmin_k::insert
+                key = dd;
+                best = s;
+            }
+            bool found = false;
+            while (sp > 0) {  // back up: the far child is visited iff box' < max_key
+                --sp;
+                if (st_box[sp] < key) {
+                    h = st_h[sp];
+                    s = st_s[sp];
+                    n = st_n[sp];
+                    cur_box = st_box[sp];
+                    found = true;
+                    break;
+                }
+            }
+            if (!found) break;
+            continue;
+        }
+        const int half = n >> 1;
+        const float qc = q[sh.t.cd[h]];
+        const float cut = fsub(qc, sh.t.cv[h]);
+        float bd;
+        if (cut < 0.0f) {  // ANNkd_split::ann_search: near child first, far child + box' stacked
+            bd = fsub(sh.t.lo[h], qc);
+            st_h[sp] = 2 * h + 2;
+            st_s[sp] = s + half;
+            st_n[sp] = n - half;
+            h = 2 * h + 1;
+            n = half;
+        } else {
+            bd = fsub(qc, sh.t.hi[h]);
+            st_h[sp] = 2 * h + 1;
+            st_s[sp] = s;
+            st_n[sp] = half;
+            h = 2 * h + 2;
+            s += half;
+            n -= half;
+        }
+        if (bd < 0.0f) bd = 0.0f;
+        st_box[sp] = fadd(cur_box, fsub(fmul(cut, cut), fmul(bd, bd)));
+        ++sp;
+    }
+    out_pos = best;
+    out_key = key;
 }
 
 // fold published log entries into the owners' registers
@@ -1322,10 +1426,28 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     if constexpr (NWG == 2) {
         if (pass == 0) pair_barrier(xp, tid);  // workgroup 1 reads prev_cnt below: workgroup 0 wrote it
     }
+    // NaN rows (yakmo's 0/0 means of seeds that won no point) stay NaN in every
+    // pass and finite rows stay finite (c + (x - c) * rate): their leaves carry
+    // +inf distances here (inert in ANN's DFS once a real leaf was reached) and
+    // the queries whose descent reaches one first take it (a2_group)
+    for (int w = tid; w < kMaxK / 32; w += nthreads) sh.nanid[w] = 0u;
     __syncthreads();
+    int nan_rows = 0;
+    for (int k = tid; k < Kr; k += nthreads) {
+        bool nn = false;
+#pragma unroll
+        for (int d = 0; d < D; ++d) nn |= C_[(int64_t)k * D + d] != C_[(int64_t)k * D + d];
+        if (nn) {
+            atomicOr(&sh.nanid[k >> 5], 1u << (k & 31));
+            nan_rows = 1;
+        }
+    }
+    nan_rows = __syncthreads_or(nan_rows);
     if (padded) {
         build_tree<D>(sh.t, sh.dist, C_, Kr);  // ANN's n/2 splits over the real centroids
         pad_tree<C::LOGK>(sh.t, reinterpret_cast<int*>(sh.dist), Kr, tid, nthreads);
+    } else if (nan_rows) {
+        build_tree<D>(sh.t, sh.dist, C_, K);  // NaN coordinates: annMaxSpread's and quickselect's exact order
     } else if (!build_tree_fast<D, C::LOGK, nthreads>(sh.t, sh.dist, sh.dfs_inc, C_, &sh.slow_pos)) {
         build_tree<D>(sh.t, sh.dist, C_, K);  // median ties: quickselect's exact order
         if (tid == 0 && wg0) frp->tree_exact += 1;
@@ -1347,7 +1469,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     for (int s = 0; s < SL; ++s) {
         const int p = p0 + s;
         const int id = p < K ? (int)sh.t.pidx[p] : 0xFFFF;
-        if (id != 0xFFFF) {
+        if (id != 0xFFFF && !((sh.nanid[id >> 5] >> (id & 31)) & 1u)) {
 #pragma unroll
             for (int d = 0; d < C::DR; ++d) {
                 creg[s][d] = C_[(int64_t)id * D + d];
@@ -1368,7 +1490,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
 #pragma unroll
             for (int d = 0; d < C::DR; ++d) creg[s][d] = 0.0f;
         }
-        cn[s] = id != 0xFFFF ? norm2_x<C::DR>(creg[s]) : __builtin_inff();
+        cn[s] = (dmask >> s) & 1u ? __builtin_inff() : norm2_x<C::DR>(creg[s]);
     }
     if constexpr (PRUNE) {  // the half-dimension bound's inputs: H-norm maxima, tail box of the centroids
         float mh = 0.0f;
@@ -1595,7 +1717,8 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             STAMP(8)
 #pragma unroll 1
             for (int j0 = wave * 4; j0 < cur_n; j0 += 4 * NWL)
-                a2_group<C, true>(sh, j0, cur_n, sh.q[cur_buf], sh.qrec[cur_buf], 0, nullptr, lane, half, twh, te
+                a2_group<C, true>(sh, j0, cur_n, sh.q[cur_buf], sh.qrec[cur_buf], 0, nullptr, lane, half, twh, te,
+                                  nan_rows != 0
 #ifdef GSC_STAMPS
                                   , acc, &tlast
 #endif
@@ -1669,7 +1792,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             const QRecT<D>& R = sh.qrec[P_buf][P_off + (cj ? j : 0)];
             // the last committed update of each centroid becomes its log entry:
             // the entry already holding that centroid, else the r-th free entry
-            const bool lastc = cj && sh.nxt[j] >= k;
+            const bool lastc = cj && sh.nxt[j] >= k && R.pad_ == 0;
             int tgt = lastc ? sh.ient[j] : -1;
             const uint64_t need = __ballot(lastc && tgt < 0);
             const uint64_t freem = __ballot(lg_pos < 0);
@@ -1811,7 +1934,16 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 // the centroid registers stay live across the DFS (it needs ~40 more
                 // VGPRs; parking the 128 in C and reloading them cost 2x the DFS time)
                 lds_barrier();  // sh.dist complete
-                dfs_parallel<C>(sh, tid, lane, wave, bpos, key);
+                if (nan_rows) {
+                    // NaN leaves carry +inf here: inert, as the query's descent
+                    // reaches a real leaf first (NaN-first queries never fail)
+                    if (tid == 0) dfs_exact_lds<C>(sh, sh.slow_pos, sh.slow_key);
+                    lds_barrier();
+                    bpos = sh.slow_pos;
+                    key = sh.slow_key;
+                } else {
+                    dfs_parallel<C>(sh, tid, lane, wave, bpos, key);
+                }
                 bpos = uniform_int(bpos);
                 ++slow_total;
                 STAMP(11)
@@ -1994,7 +2126,8 @@ extern "C" hipError_t gsc_launch_scan_batch(int D, int logk, ReduceFrame* frames
     SB(16, 8, 4, 1) SB(16, 9, 4, 1) SB(16, 10, 4, 1) SB(16, 11, 4, 1) SB(16, 12, 8, 1)
     SB(32, 8, 4, 1) SB(32, 9, 4, 1) SB(32, 10, 4, 1) SB(32, 11, 4, 1)
     // D = 32, K = 4096: one CU per frame, the DCT half of every centroid in
-    // VGPRs and the cepstrum half in the frame's tail array (split layout)
+    // VGPRs and the cepstrum half in the frame's tail array (split layout;
+    // measured at D = 16 too: 4294 vs 4309 ms at the C2 bench shape, not kept)
     if (D == 32 && logk == 12)
         return launch_scan<ScanCfg<32, 12, 8, 1, 16>>(frames, nframes, X, Cc, is, rate_tab, tol, max_passes, xbuf,
                                                       opts, tails, st);
@@ -2005,4 +2138,6 @@ extern "C" hipError_t gsc_launch_scan_batch(int D, int logk, ReduceFrame* frames
 extern "C" size_t gsc_scan_xbuf_granules_per_frame(void) { return 2 * 2 * (size_t)kXCap; }
 
 // floats of the split layout's tail array per frame (0: the shape keeps every feature in VGPRs)
-extern "C" size_t gsc_scan_tail_floats_per_frame(int D, int logk) { return D == 32 && logk == 12 ? 4096 * 16 : 0; }
+extern "C" size_t gsc_scan_tail_floats_per_frame(int D, int logk) {
+    return logk == 12 && D == 32 ? 4096 * size_t(D / 2) : 0;
+}
