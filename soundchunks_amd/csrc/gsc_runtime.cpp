@@ -350,6 +350,14 @@ int run_reduce_batch_dev(int D, int K, int precision, const std::vector<int>& Ns
                          at(0.0), at(0.1), at(0.5), at(0.9));
         }
     }
+    if (std::getenv("GSC_FRAME_STATS")) {  // diagnostic: per-frame chain length and finishing time
+        uint64_t t0 = ~0ull;
+        for (int i = 0; i < nf; ++i)
+            if (fr[i].t_done) t0 = std::min<uint64_t>(t0, fr[i].t_done);
+        for (int i = 0; i < nf; ++i)
+            std::fprintf(stderr, "frame %d: N %d passes %d slow %d restarts %d done +%.1f ms\n", i, fr[i].N, fr[i].iters,
+                         fr[i].slow, fr[i].restarts, fr[i].t_done ? double(fr[i].t_done - t0) / 1e5 : -1.0);
+    }
     if (std::getenv("GSC_HOST_TIMING") && nf > 0 && fr[0].ystamps[6] + fr[0].ystamps[1] + fr[0].ystamps[2] != 0) {
         // stamps builds: yakmo phase clocks, mean over frames (cycles per pick)
         double m[16] = {};

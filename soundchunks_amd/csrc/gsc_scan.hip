@@ -1457,7 +1457,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     float cn[SL];  // |c|^2 (over the register features) per register leaf (A1 bounds); +inf for padding leaves
     const int p0 = (vwave * 64 + lane) * SL;
     bool nan_here = false;
-    uint32_t dmask = 0;  // slots that hold no centroid (past K, or padding leaves)
+    uint32_t dmask = 0;  // slots that hold no live centroid (past K, padding, NaN rows, dead leaves): +inf distances
     constexpr int TLA = C::TL > 0 ? C::TL : 1;
     float tlo[TLA], thi[TLA];  // split layout: this lane's tail box
 #pragma unroll
@@ -1469,7 +1469,19 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     for (int s = 0; s < SL; ++s) {
         const int p = p0 + s;
         const int id = p < K ? (int)sh.t.pidx[p] : 0xFFFF;
-        if (id != 0xFFFF && !((sh.nanid[id >> 5] >> (id & 31)) & 1u)) {
+        // NaN passes: a split node with a NaN cut value sends every query to
+        // its high child first and never enters the low one (box' = NaN), so
+        // the leaves below a low child of such a node are dead for the pass
+        bool dead = false;
+        if (nan_rows && p < K) {
+#pragma unroll 1
+            for (int l = 0, h = 0; l < C::LOGK; ++l) {
+                const int bit = (p >> (C::LOGK - 1 - l)) & 1;
+                dead |= bit == 0 && sh.t.cv[h] != sh.t.cv[h];
+                h = 2 * h + 1 + bit;
+            }
+        }
+        if (id != 0xFFFF && !dead && !((sh.nanid[id >> 5] >> (id & 31)) & 1u)) {
 #pragma unroll
             for (int d = 0; d < C::DR; ++d) {
                 creg[s][d] = C_[(int64_t)id * D + d];
