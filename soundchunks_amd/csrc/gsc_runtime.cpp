@@ -2,6 +2,7 @@
 // batched launches of the Reduce (yakmo + KNNScanReduce) and KNNFit kernels
 // over many frames at once, host thread pool for the per-frame DSP, and the
 // C ABI declared in include/soundchunks.h.
+#include <cstddef>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -231,24 +232,33 @@ hipError_t launch_scan_passes(int D, ReduceFrame* dfr, int nf, int K, const floa
     // every launch advances each live frame by at least one pass (the batched
     // kernel runs a frame until it converges or meets a NaN pass, which the
     // generic launch then takes), so max_passes rounds always suffice
-    std::vector<int32_t> done(static_cast<size_t>(nf));
+    std::vector<int32_t> flags(2 * static_cast<size_t>(nf));  // (done, generic) per frame
+    static_assert(offsetof(ReduceFrame, generic) == offsetof(ReduceFrame, done) + sizeof(int32_t), "adjacent flags");
     for (int round = 0; round < max_passes; ++round) {
         if (batched) {
             // opts bit 0 (diagnostic GSC_SCAN_FULL_A1): full-dimension A1 bounds in every pass
             const int opts = std::getenv("GSC_SCAN_FULL_A1") ? 1 : 0;
-            const hipError_t e =
+            hipError_t e =
                 gsc_launch_scan_batch(D, logk, dfr, nf, X, C, is, rate, tol, max_passes, xbuf.p, opts, tails.p, nullptr);
             if (e != hipSuccess) return e;
+            // the generic kernel runs only when the batched one handed a frame
+            // over (an empty launch of it still costs ~30 ms: 256 large-LDS
+            // workgroups); stop once every frame is done
+            e = hipMemcpy2D(flags.data(), 2 * sizeof(int32_t), &dfr[0].done, sizeof(ReduceFrame), 2 * sizeof(int32_t),
+                            size_t(nf), hipMemcpyDeviceToHost);
+            if (e != hipSuccess) return e;
+            g_scan_rounds.fetch_add(1);
+            bool any_generic = false, all_done = true;
+            for (int i = 0; i < nf; ++i) {
+                all_done = all_done && flags[2 * size_t(i)] != 0;
+                any_generic = any_generic || flags[2 * size_t(i) + 1] != 0;
+            }
+            if (all_done) break;
+            if (!any_generic) continue;
         }
         const hipError_t e = gsc_launch_scan_pass(D, dfr, nf, K, X, C, is, fs, rate, tol, max_passes, batched ? 1 : 0, nullptr);
         if (e != hipSuccess) return e;
-        g_scan_rounds.fetch_add(1);
-        if (!batched) continue;  // the generic kernel runs one pass per round
-        // stop once every frame is done (read back the done flags only)
-        const hipError_t c = hipMemcpy2D(done.data(), sizeof(int32_t), &dfr[0].done, sizeof(ReduceFrame),
-                                         sizeof(int32_t), size_t(nf), hipMemcpyDeviceToHost);
-        if (c != hipSuccess) return c;
-        if (std::all_of(done.begin(), done.end(), [](int32_t v) { return v != 0; })) break;
+        if (!batched) g_scan_rounds.fetch_add(1);  // the generic kernel runs one pass per round
     }
     return hipSuccess;
 }

@@ -1,17 +1,12 @@
 #!/bin/bash
 # Round-3 profile set (one gpurun call): kernel trace + stats of the default bench (C2, 1024 s),
 # FETCH_SIZE and WRITE_SIZE PMC passes (separate runs, 256 s / 64 frames), then the default
-# bench with its CPU baseline leg, and the C3 bench with its baseline.
-set -o pipefail
+# bench with its CPU baseline leg.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/prof3
+O=gpurun_out/prof
 mkdir -p $O
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/trace.log 2>&1 &&
-timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o run -- python3 -u bench.py --seconds 256 --steps 1 --warmup 0 --no-cpu-baseline > $O/fetch.log 2>&1 &&
-timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $O/write -o run -- python3 -u bench.py --seconds 256 --steps 1 --warmup 0 --no-cpu-baseline > $O/write.log 2>&1 &&
-timeout -k 10 400 python3 -u bench.py > $O/bench_default.log 2>&1 &&
-timeout -k 10 400 python3 -u bench.py --config c3 > $O/bench_c3.log 2>&1
-rc=$?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run -- python3 -u bench.py --steps 1 --warmup 0 --no-cpu-baseline > $O/trace.log 2>&1 || exit 2
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o run -- python3 -u bench.py --seconds 256 --steps 1 --warmup 0 --no-cpu-baseline > $O/fetch.log 2>&1 || exit 3
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $O/write -o run -- python3 -u bench.py --seconds 256 --steps 1 --warmup 0 --no-cpu-baseline > $O/write.log 2>&1 || exit 4
+timeout -k 10 400 python3 -u bench.py > $O/bench_default.log 2>&1 || exit 5
 tail -1 $O/bench_default.log | cut -c1-300
-tail -1 $O/bench_c3.log | cut -c1-300
-exit $rc
