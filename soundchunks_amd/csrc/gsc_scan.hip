@@ -68,7 +68,7 @@ struct ScanCfg {
     static constexpr int DR = DR_, TL = D_ - DR_;
     static constexpr bool SPLIT = TL > 0;
     static constexpr int K = 1 << LOGK;
-    static constexpr int LS = SL == 8 ? 3 : (SL == 4 ? 2 : 1);        // log2 slots per lane
+    static constexpr int LS = SL == 8 ? 3 : (SL == 4 ? 2 : (SL == 2 ? 1 : 0));  // log2 slots per lane
     static constexpr int LPW = 64 * SL;                                 // leaves per wave
     static constexpr int KG = K / NWG;                                  // leaves per workgroup
     static constexpr bool FULL = KG >= LPW;                             // every lane holds SL leaves
@@ -131,13 +131,18 @@ __device__ __forceinline__ int rec_slot(const WaveRecT<SL>& r, bool* tie2) {
 template <int SL>
 __device__ __forceinline__ uint32_t rec_sib(const WaveRecT<SL>& r, int ls, int idx) {
     if (idx < 6) return keybits((int)r.sl[idx]);
-    if (idx == 6) return r.b[ls ^ 1];
-    if (SL == 4 || idx == 7) {
-        const int pb = (ls & (SL - 4)) | ((ls & 2) ^ 2);
-        return fminb(r.b[pb], r.b[pb + 1]);
+    if constexpr (SL >= 2) {
+        if (idx == 6) return r.b[ls ^ 1];
     }
-    const int qb = (ls & 4) ^ 4;
-    return fminb(fminb(r.b[qb], r.b[qb + 1]), fminb(r.b[qb + 2], r.b[qb + 3]));
+    if constexpr (SL >= 4) {
+        if (SL == 4 || idx == 7) {
+            const int pb = (ls & (SL - 4)) | ((ls & 2) ^ 2);
+            return fminb(r.b[pb], r.b[pb + 1]);
+        }
+        const int qb = (ls & 4) ^ 4;
+        return fminb(fminb(r.b[qb], r.b[qb + 1]), fminb(r.b[qb + 2], r.b[qb + 3]));
+    }
+    return kInfBits;  // no slot levels below SL
 }
 
 template <int D>
@@ -460,13 +465,19 @@ __device__ __forceinline__ A1Tree<C::SL> a1_tree(const float (&dv)[C::SL], int v
     const bool has = C::FULL || p0 < C::K;  // small K: only the low lanes hold leaves
 #pragma unroll
     for (int s = 0; s < SL; ++s) t.b[s] = has ? __float_as_uint(dv[s]) : kInfBits;
-    uint32_t mm[SL / 2];
-#pragma unroll
-    for (int s = 0; s < SL / 2; ++s) mm[s] = fminb(t.b[2 * s], t.b[2 * s + 1]);
-    if constexpr (SL == 8) {
-        t.lmin = fminb(fminb(mm[0], mm[1]), fminb(mm[2], mm[3]));
+    if constexpr (SL == 1) {
+        t.lmin = t.b[0];
     } else {
-        t.lmin = fminb(mm[0], mm[1]);
+        uint32_t mm[SL / 2];
+#pragma unroll
+        for (int s = 0; s < SL / 2; ++s) mm[s] = fminb(t.b[2 * s], t.b[2 * s + 1]);
+        if constexpr (SL == 8) {
+            t.lmin = fminb(fminb(mm[0], mm[1]), fminb(mm[2], mm[3]));
+        } else if constexpr (SL == 4) {
+            t.lmin = fminb(mm[0], mm[1]);
+        } else {
+            t.lmin = mm[0];
+        }
     }
     // wave min-tree on order keys: partner group minima are the sibling subtrees on the path
     const int key = ordkey(t.lmin);
@@ -1448,6 +1459,8 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         pad_tree<C::LOGK>(sh.t, reinterpret_cast<int*>(sh.dist), Kr, tid, nthreads);
     } else if (nan_rows) {
         build_tree<D>(sh.t, sh.dist, C_, K);  // NaN coordinates: annMaxSpread's and quickselect's exact order
+    } else if constexpr (K / nthreads < 4) {
+        build_tree<D>(sh.t, sh.dist, C_, K);  // one or two leaves per thread: the sequential build
     } else if (!build_tree_fast<D, C::LOGK, nthreads>(sh.t, sh.dist, sh.dfs_inc, C_, &sh.slow_pos)) {
         build_tree<D>(sh.t, sh.dist, C_, K);  // median ties: quickselect's exact order
         if (tid == 0 && wg0) frp->tree_exact += 1;
@@ -2132,11 +2145,13 @@ extern "C" hipError_t gsc_launch_scan_batch(int D, int logk, ReduceFrame* frames
     if (D == DV && logk == LK)                                                                                 \
         return launch_scan<ScanCfg<DV, LK, SLV, NG>>(frames, nframes, X, Cc, is, rate_tab, tol, max_passes, xbuf, \
                                                      opts, tails, st);
-    // K below 4096: four leaves per lane, so a frame gets twice the waves
-    // (K = 512: two instead of one); the per-search work there is latency
-    SB(8, 8, 4, 1) SB(8, 9, 4, 1) SB(8, 10, 4, 1) SB(8, 11, 4, 1) SB(8, 12, 8, 1)
-    SB(16, 8, 4, 1) SB(16, 9, 4, 1) SB(16, 10, 4, 1) SB(16, 11, 4, 1) SB(16, 12, 8, 1)
-    SB(32, 8, 4, 1) SB(32, 9, 4, 1) SB(32, 10, 4, 1) SB(32, 11, 4, 1)
+    // K below 4096: fewer leaves per lane, so a frame keeps (up to) 8 waves --
+    // the per-search work there is latency (A2 certificates, V checks and the
+    // commit spread over the waves): K = 256 / 512 one leaf per lane (4 / 8
+    // waves), K = 1024 two, K = 2048 four
+    SB(8, 8, 1, 1) SB(8, 9, 1, 1) SB(8, 10, 2, 1) SB(8, 11, 4, 1) SB(8, 12, 8, 1)
+    SB(16, 8, 1, 1) SB(16, 9, 1, 1) SB(16, 10, 2, 1) SB(16, 11, 4, 1) SB(16, 12, 8, 1)
+    SB(32, 8, 1, 1) SB(32, 9, 1, 1) SB(32, 10, 2, 1) SB(32, 11, 4, 1)
     // D = 32, K = 4096: one CU per frame, the DCT half of every centroid in
     // VGPRs and the cepstrum half in the frame's tail array (split layout;
     // measured at D = 16 too: 4294 vs 4309 ms at the C2 bench shape, not kept)
