@@ -237,7 +237,8 @@ hipError_t launch_scan_passes(int D, ReduceFrame* dfr, int nf, int K, const floa
     for (int round = 0; round < max_passes; ++round) {
         if (batched) {
             // opts bit 0 (diagnostic GSC_SCAN_FULL_A1): full-dimension A1 bounds in every pass
-            const int opts = std::getenv("GSC_SCAN_FULL_A1") ? 1 : 0;
+            // bit 1 (GSC_SCAN_NO_PRUNE, experiment): no per-wave A1 pruning
+            const int opts = (std::getenv("GSC_SCAN_FULL_A1") ? 1 : 0) | (std::getenv("GSC_SCAN_NO_PRUNE") ? 2 : 0);
             hipError_t e =
                 gsc_launch_scan_batch(D, logk, dfr, nf, X, C, is, rate, tol, max_passes, xbuf.p, opts, tails.p, nullptr);
             if (e != hipSuccess) return e;
@@ -1709,6 +1710,11 @@ int gsc_scan_reduce(int n, int d, const float* x, int k, float* centroids, int* 
         for (int w = 0; w < 8; ++w) {
             std::fprintf(stderr, "\n  w%d:", w);
             for (int k = 0; k < 16; ++k) std::fprintf(stderr, " %.3g", double(fr[0].stamps[w * 16 + k]));
+        }
+        std::fprintf(stderr, "\nA1 queries [home pruned evaluated | iterations fixups pending]");
+        for (int w = 0; w < 8; ++w) {
+            std::fprintf(stderr, "\n  w%d:", w);
+            for (int k = 0; k < 6; ++k) std::fprintf(stderr, " %.4g", double(fr[0].acounts[w * 8 + k]));
         }
         std::fprintf(stderr, "\n");
     }

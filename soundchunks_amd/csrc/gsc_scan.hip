@@ -1362,6 +1362,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     constexpr int kErrWave = NWL > 1 ? 1 : 0;  // residual + cluster ids (wave 0 keeps the log)
     constexpr bool PRUNE = NWG == 1;           // A1 pruning by wave boxes (one-CU frames)
     const bool no_half = (opts & 1) != 0;      // diagnostic: full-dimension A1 bounds in every pass
+    const bool no_prune = (opts & 2) != 0;     // experiment: every wave evaluates every query (no mid-A1 barrier)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Scan2Shared<C>& sh = *reinterpret_cast<Scan2Shared<C>*>(smem);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1641,6 +1642,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     bool guard = false;  // the progress guard tripped (identical in both workgroups)
 #ifdef GSC_STAMPS
     uint64_t acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t acn[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // home, pruned, evaluated, iterations, fixups, pending
     uint64_t tlast = stamp();
     acc[9] = tlast - t_kernel0;  // pass setup: tree build, registers, first queries
 #endif
@@ -1688,7 +1690,9 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         uint64_t prunedm = 0;  // queries this wave skipped (wave-uniform)
         float lbp = 0.0f, qn_j = 0.0f, eps_j = 0.0f;  // lane j: query j's box bound, |q|^2, eps
         if constexpr (PRUNE) {
-            if (cur_n > 0) {
+            if (no_prune) {
+                a1_mask(curm);
+            } else if (cur_n > 0) {
                 const int jr = lane < cur_n ? lane : 0;
                 const float* qv = sh.q[cur_buf][jr];
                 lbp = wave_box_lb<C>(sh, qv, vwave);
@@ -1712,6 +1716,11 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 const float ubj = __uint_as_float(sh.ub[jr]);
                 const float thr = fmul(fadd(ubj, fmul(4.0f, eps_j)), 1.0f + 0x1p-20f);
                 prunedm = __ballot(lbp > thr) & curm & ~home;
+#ifdef GSC_STAMPS
+                acn[0] += __popcll(home);
+                acn[1] += __popcll(prunedm);
+                acn[2] += __popcll(curm & ~home & ~prunedm);
+#endif
                 if ((prunedm >> lane) & 1ull)  // a lower bound of this wave's A1 values (see above)
                     sh.wrec[vwave][lane].minbits = __float_as_uint(fsub(fsub(lbp, fmul(3.0f, eps_j)), qn_j));
                 a1_mask(curm & ~home & ~prunedm);
@@ -1720,6 +1729,10 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             a1_mask(curm);
         }
         if (wave == 0 && has_p) vp_end<C>(sh, P_buf, P_off, P_n, lane, lg_pos, vst);
+#ifdef GSC_STAMPS
+        acn[3] += 1;
+        acn[5] += P_n;
+#endif
         STAMP(1)
         lds_barrier();
         STAMP(6)
@@ -1757,6 +1770,9 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             const uint64_t fx = __ballot(lane < cur_n && sh.qrec[cur_buf][lane].valid == 0);
             if (fx) {
                 const int nfx = __popcll(fx);
+#ifdef GSC_STAMPS
+                acn[4] += nfx;
+#endif
                 if (wave == 0 && ((fx >> lane) & 1ull)) sh.fxl[__popcll(fx & ((1ull << lane) - 1ull))] = lane;
                 uint64_t m = fx;
                 while (m) {
@@ -2062,6 +2078,8 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
 #ifdef GSC_STAMPS
     if (lane == 0 && wg0)
         for (int k = 0; k < 16; ++k) frp->stamps[wave * 16 + k] += acc[k];
+    if (lane == 0 && wg0)
+        for (int k = 0; k < 8; ++k) frp->acounts[wave * 8 + k] += acn[k];
 #endif
     const double diff = err > prev_err ? err - prev_err : prev_err - err;
     const bool done = diff <= tol || pass + 1 >= kMaxScanIters || guard;

@@ -18,10 +18,11 @@ from soundchunks_amd.synth import synth_wav  # noqa: E402
 
 passes = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 cs = int(sys.argv[2]) if len(sys.argv) > 2 else 8
-argv = [f"-cs{cs}", "-cpf4096", "-cbd8"]
+k = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
+argv = [f"-cs{cs}", f"-cpf{k}", "-cbd8"]
 wav = synth_wav(8.0)
 att, feat = sc.frame_dsp(wav, 0, argv)
-y = sc.yakmo_seed_means(feat, 4096)
+y = sc.yakmo_seed_means(feat, k)
 os.environ["GSC_SCAN_MAX_PASSES"] = str(passes)
 t = time.time()
 c, cl, it = sc.scan_reduce(feat, y, 3)
