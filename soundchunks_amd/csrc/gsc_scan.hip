@@ -792,6 +792,37 @@ __device__ __forceinline__ void a2_group(Scan2Shared<C>& sh, int j0, int nq, con
         ok = !far || (fsub(fadd(qn, __uint_as_float(sib)), eps) > Bv);
         unique = fsub(__uint_as_float(m2), __uint_as_float(gmin)) > fadd(eps, eps);
         m2lo = fsub(fadd(qn, __uint_as_float(m2)), eps);
+        const bool gfail = !unique || ((__ballot(!ok) >> gbase) & 0xFFFFull) != 0;
+        if (__ballot(gfail) != 0) {
+            // a query of this wave failed with the frame-wide bound: retry with an
+            // error bound per wave.  A leaf of wave w has |c|^2 <= cnmax[w]
+            // (monotone within the pass, so it covers any earlier snapshot), so its
+            // A1 value is within eps_w = (|q|^2 + cnmax[w]) EPSF (+ TE) of the
+            // reference's distance: quiet queries among quiet centroids get their
+            // own scale instead of the frame's loudest centroid's
+            auto epsw = [&](int w) { return fadd(fadd(fmul(fadd(qn0, sh.cnmax[w]), C::EPSF), 1e-37f), te); };
+            const float eW = epsw(Wv);
+            float eS = eW;  // the sibling subtree's bound: its waves' (wave-level depths) or W's
+            if (l < KW) {
+                const int sh_ = KW - 1 - l;
+                const int want = (W >> sh_) ^ 1;
+                eS = 0.0f;
+#pragma unroll
+                for (int w = 0; w < NW; ++w)
+                    if ((w >> sh_) == want) eS = fmaxf(eS, epsw(w));
+            }
+            ok = !far || (fsub(fadd(qn, __uint_as_float(sib)), eS) > Bv);
+            // c* beats every other leaf: W's own other leaves (lane / slot depths)
+            // and every other wave's minimum, each with its wave's bound
+            const float gm = __uint_as_float(gmin);
+            const float m2W = __uint_as_float(fmin16((l >= KW && l < LOGK) ? sib : kInfBits));
+            const bool ow = l < NW && l != Wv;  // lane l: another wave's record
+            const float el = ow ? epsw(l) : 0.0f;
+            const bool uw = !ow || fsub(__uint_as_float(mw), gm) > fadd(eW, el);
+            unique = fsub(m2W, gm) > fadd(eW, eW) && ((__ballot(!uw) >> gbase) & 0xFFFFull) == 0;
+            const float lo_l = ow ? fsub(fadd(qn, __uint_as_float(mw)), el) : __builtin_inff();
+            m2lo = fminf(fsub(fadd(qn, m2W), eW), __uint_as_float(fmin16(__float_as_uint(lo_l))));
+        }
     } else {
         ok = !far || (__uint_as_float(sib) > Bv);
         unique = !tie;
@@ -1458,8 +1489,11 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     if (padded) {
         build_tree<D>(sh.t, sh.dist, C_, Kr);  // ANN's n/2 splits over the real centroids
         pad_tree<C::LOGK>(sh.t, reinterpret_cast<int*>(sh.dist), Kr, tid, nthreads);
-    } else if (nan_rows) {
-        build_tree<D>(sh.t, sh.dist, C_, K);  // NaN coordinates: annMaxSpread's and quickselect's exact order
+    } else if (nan_rows) {  // NaN coordinates: annMaxSpread's and quickselect's exact order
+        if constexpr (K / nthreads >= 4)
+            build_tree_nan<D, C::LOGK, nthreads>(sh.t, sh.dist, sh.dfs_inc, C_);
+        else
+            build_tree<D>(sh.t, sh.dist, C_, K);
     } else if constexpr (K / nthreads < 4) {
         build_tree<D>(sh.t, sh.dist, C_, K);  // one or two leaves per thread: the sequential build
     } else if (!build_tree_fast<D, C::LOGK, nthreads>(sh.t, sh.dist, sh.dfs_inc, C_, &sh.slow_pos)) {

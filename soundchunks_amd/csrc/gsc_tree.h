@@ -215,6 +215,197 @@ __device__ bool build_tree_fast(KdTree& t, float* __restrict__ val, float* __res
     return *tie == 0;
 }
 
+// annMedianSplit (ANN.dll @0x180015680) on one node's segment, one thread:
+// quickselect of the n_lo = n/2 smallest cut-dimension values (pidx and their
+// staged values val move together; NaN values compare false everywhere, as in
+// the DLL), then the largest of the low side moved to n_lo - 1
+__device__ __forceinline__ void median_split(uint16_t* __restrict__ pidx, float* __restrict__ val, int n) {
+    const int n_lo = n >> 1;
+    int l = 0, r = n - 1;
+#define PSWAP(a, b)                 \
+    {                               \
+        const uint16_t t_ = pidx[a]; \
+        pidx[a] = pidx[b];          \
+        pidx[b] = t_;               \
+        const float v_ = val[a];    \
+        val[a] = val[b];            \
+        val[b] = v_;                \
+    }
+    while (l < r) {
+        int i = (r + l) / 2;
+        int k;
+        if (val[i] > val[r]) PSWAP(i, r)
+        PSWAP(l, i);
+        const float c = val[l];
+        i = l;
+        k = r;
+        for (;;) {
+            while (val[++i] < c) {}
+            while (val[--k] > c) {}
+            if (i < k) PSWAP(i, k) else break;
+        }
+        PSWAP(l, k);
+        if (k > n_lo) r = k - 1;
+        else if (k < n_lo) l = k + 1;
+        else break;
+    }
+    if (n_lo > 0) {
+        float c = val[0];
+        int k = 0;
+        for (int i = 1; i < n_lo; ++i)
+            if (val[i] > c) {
+                c = val[i];
+                k = i;
+            }
+        PSWAP(n_lo - 1, k);
+    }
+#undef PSWAP
+}
+
+// ---------------------------------------------------------------------------
+// Exact build for K = 2^LOGK centroids some of which are NaN (yakmo's 0/0
+// means): quickselect's order matters there (NaN compares false), so each
+// node's median split runs sequentially on one thread (median_split, as in
+// build_tree) -- but on cut values staged in LDS by all threads, and with the
+// node spreads computed by all threads.  annMaxSpread's sequential min / max
+// start at the segment's first point and never take a NaN, so per dimension
+// the spread is NaN (never the cut dimension) when the first point's value is
+// NaN, else max - min over the non-NaN values (fminf / fmaxf skip NaN); the
+// enclosing rectangle likewise starts at point 0.
+//   val: K floats of LDS scratch; red: 2*D*(K/512) floats of LDS scratch.
+// ---------------------------------------------------------------------------
+template <int D, int LOGK, int NT>
+__device__ void build_tree_nan(KdTree& t, float* __restrict__ val, float* __restrict__ red,
+                               const float* __restrict__ C) {
+    constexpr int K = 1 << LOGK;
+    constexpr int PT = K / NT;  // kd-leaf positions per thread
+    static_assert(PT * NT == K && (PT == 4 || PT == 8), "positions per thread");
+    const int tid = threadIdx.x, wave = tid >> 6;
+    const int p0 = tid * PT;
+    for (int p = tid; p < K; p += NT) t.pidx[p] = (uint16_t)p;
+    __syncthreads();
+    // cut dimension of the node whose segment starts at position sb, from its min / max
+    auto pick = [&](int sb, const float (&mn)[D], const float (&mx)[D]) {
+        const float* f = C + (int64_t)t.pidx[sb] * D;  // the segment's first point
+        int cdim = 0;
+        float max_spr = 0.0f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const float spr = f[d] != f[d] ? f[d] : fsub(mx[d], mn[d]);
+            if (spr > max_spr) {
+                max_spr = spr;
+                cdim = d;
+            }
+        }
+        return cdim;
+    };
+    for (int L = 0; L < LOGK; ++L) {
+        const int S = K >> L;
+        const int first = (1 << L) - 1;
+        if (S >= PT) {
+            float mn[D], mx[D];
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                mn[d] = __builtin_nanf("");
+                mx[d] = __builtin_nanf("");
+            }
+#pragma unroll
+            for (int i = 0; i < PT; ++i) {
+                const float* r = C + (int64_t)t.pidx[p0 + i] * D;
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    mn[d] = fminf(mn[d], r[d]);
+                    mx[d] = fmaxf(mx[d], r[d]);
+                }
+            }
+            const int G = S / PT;
+            const int GW = G < 64 ? G : 64;
+            for (int o = 1; o < GW; o <<= 1) {
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    mn[d] = fminf(mn[d], __shfl_xor(mn[d], o));
+                    mx[d] = fmaxf(mx[d], __shfl_xor(mx[d], o));
+                }
+            }
+            if (G > 64) {
+                if ((tid & 63) == 0) {
+#pragma unroll
+                    for (int d = 0; d < D; ++d) {
+                        red[wave * 2 * D + d] = mn[d];
+                        red[wave * 2 * D + D + d] = mx[d];
+                    }
+                }
+                __syncthreads();
+                const int wn = G / 64, w0 = (wave / wn) * wn;
+                for (int w = w0; w < w0 + wn; ++w) {
+#pragma unroll
+                    for (int d = 0; d < D; ++d) {
+                        mn[d] = fminf(mn[d], red[w * 2 * D + d]);
+                        mx[d] = fmaxf(mx[d], red[w * 2 * D + D + d]);
+                    }
+                }
+            }
+            if (p0 % S == 0) {
+                t.cd[first + p0 / S] = (uint8_t)pick(p0, mn, mx);
+                if (L == 0) {  // annEnclRect from point 0
+#pragma unroll
+                    for (int d = 0; d < D; ++d) {
+                        const float c0 = C[d];
+                        t.bnd_lo[d] = c0 != c0 ? c0 : mn[d];
+                        t.bnd_hi[d] = c0 != c0 ? c0 : mx[d];
+                    }
+                }
+            }
+        } else {
+            for (int g = 0; g < PT / S; ++g) {
+                float mn[D], mx[D];
+                const int pb = p0 + g * S;
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    mn[d] = __builtin_nanf("");
+                    mx[d] = __builtin_nanf("");
+                }
+                for (int i = 0; i < S; ++i) {
+                    const float* r = C + (int64_t)t.pidx[pb + i] * D;
+#pragma unroll
+                    for (int d = 0; d < D; ++d) {
+                        mn[d] = fminf(mn[d], r[d]);
+                        mx[d] = fmaxf(mx[d], r[d]);
+                    }
+                }
+                t.cd[first + pb / S] = (uint8_t)pick(pb, mn, mx);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < PT; ++i) {  // cut-dimension values, staged in LDS
+            const int p = p0 + i;
+            val[p] = C[(int64_t)t.pidx[p] * D + t.cd[first + p / S]];
+        }
+        __syncthreads();
+        for (int node = tid; node < (1 << L); node += NT) {  // quickselect, one thread per node
+            const int h = first + node, sb = node * S, nl = S >> 1;
+            median_split(t.pidx + sb, val + sb, S);
+            const int cdim = t.cd[h];
+            float lov = t.bnd_lo[cdim], hiv = t.bnd_hi[cdim];
+            int a = 0;
+            const int path = h + 1;
+            for (int bl = L - 1; bl >= 0; --bl) {
+                const int right = (path >> bl) & 1;
+                if (t.cd[a] == cdim) {
+                    if (right) lov = t.cv[a];
+                    else hiv = t.cv[a];
+                }
+                a = 2 * a + 1 + right;
+            }
+            t.cv[h] = (float)((double)fadd(val[sb + nl - 1], val[sb + nl]) / 2.0);
+            t.lo[h] = lov;
+            t.hi[h] = hiv;
+        }
+        __syncthreads();
+    }
+}
+
 // segment of heap node h (root 0, children 2h+1 / 2h+2, n_lo = n/2)
 __device__ __forceinline__ void node_segment(int h, int K, int& s, int& n, int& depth) {
     s = 0;
@@ -339,46 +530,7 @@ __device__ void build_tree(KdTree& sh, float* __restrict__ scratch, const float*
             float* val = scratch + s;  // cut-dim values of the segment
             for (int i = 0; i < n; ++i) val[i] = C[(int64_t)pidx[i] * D + cdim];
             const int n_lo = n >> 1;
-            // annMedianSplit (ANN.dll @0x180015680)
-            int l = 0, r = n - 1;
-#define PSWAP(a, b)                 \
-    {                               \
-        const uint16_t t_ = pidx[a]; \
-        pidx[a] = pidx[b];          \
-        pidx[b] = t_;               \
-        const float v_ = val[a];    \
-        val[a] = val[b];            \
-        val[b] = v_;                \
-    }
-            while (l < r) {
-                int i = (r + l) / 2;
-                int k;
-                if (val[i] > val[r]) PSWAP(i, r)
-                PSWAP(l, i);
-                const float c = val[l];
-                i = l;
-                k = r;
-                for (;;) {
-                    while (val[++i] < c) {}
-                    while (val[--k] > c) {}
-                    if (i < k) PSWAP(i, k) else break;
-                }
-                PSWAP(l, k);
-                if (k > n_lo) r = k - 1;
-                else if (k < n_lo) l = k + 1;
-                else break;
-            }
-            if (n_lo > 0) {
-                float c = val[0];
-                int k = 0;
-                for (int i = 1; i < n_lo; ++i)
-                    if (val[i] > c) {
-                        c = val[i];
-                        k = i;
-                    }
-                PSWAP(n_lo - 1, k);
-            }
-#undef PSWAP
+            median_split(pidx, val, n);
             const float cvv = (float)((double)fadd(val[n_lo - 1], val[n_lo]) / 2.0);
             // node bounds: root rect narrowed by ancestors cutting the same dim
             float lov = sh.bnd_lo[cdim], hiv = sh.bnd_hi[cdim];

@@ -20,8 +20,12 @@ passes = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 cs = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 k = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
 argv = [f"-cs{cs}", f"-cpf{k}", "-cbd8"]
-wav = synth_wav(8.0)
-att, feat = sc.frame_dsp(wav, 0, argv)
+# optional: a WAV file and frame index instead of the synthetic C2 frame
+wav = Path(sys.argv[4]).read_bytes() if len(sys.argv) > 4 else synth_wav(8.0)
+frame = int(sys.argv[5]) if len(sys.argv) > 5 else 0
+if len(sys.argv) > 4:
+    argv = [f"-cs{cs}", f"-cpf{k}"]
+att, feat = sc.frame_dsp(wav, frame, argv)
 y = sc.yakmo_seed_means(feat, k)
 os.environ["GSC_SCAN_MAX_PASSES"] = str(passes)
 t = time.time()
