@@ -1701,6 +1701,9 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         }
         // ---- part 1: chain the pending batch's updates (wave 0); A1(current)
         VPState vst;
+#ifdef GSC_STAMPS_PREP
+        STAMP(14)  // diagnostic split of "prep": loop top (into a2box's slot) vs the update chain
+#endif
         if (wave == 0 && has_p) vp_begin<C>(sh, P_buf, P_off, P_n, vq_a10, lane, lg_pos, lg_tag, vst);
         STAMP(0)
         // A1 of the queries in mask m, two per trip: one query's min-tree (a

@@ -116,3 +116,26 @@ def test_generic_scan_kernel_still_exact(name):
     env = dict(os.environ, GSC_SCAN_GENERIC="1")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_scan_nan_centroids_k4096(oracle):
+    """A frame with NaN centroids (the corpus' 60.wav: yakmo 0/0 means of seeds
+    that won no point) in the batched kernel: NaN-first descents, dead low
+    children of NaN cuts, the NaN-exact tree build and the exact LDS-stack DFS,
+    first passes against the oracle (NaN rows compared as NaN)."""
+    import soundchunks_amd as sc
+
+    wav = (ROOT / "tests" / "golden" / "lame_test" / "60.wav").read_bytes()
+    t = oracle.trace_frame(wav, ["-cs8", "-cpf4096"], 1)
+    assert int(np.isnan(t["yakmo"]).any(axis=1).sum()) > 1000
+    os.environ["GSC_SCAN_MAX_PASSES"] = "3"
+    try:
+        gc, gcl, gn = sc.scan_reduce(t["dataset"], t["yakmo"], precision=3)
+    finally:
+        del os.environ["GSC_SCAN_MAX_PASSES"]
+    oc, ocl, on = oracle.scan_reduce(t["dataset"], t["yakmo"], 3, 3)
+    assert gn == on == 3
+    np.testing.assert_array_equal(gcl, ocl)
+    nan = np.isnan(oc)
+    np.testing.assert_array_equal(np.isnan(gc), nan)
+    np.testing.assert_array_equal(_bits(np.where(nan, 0, gc)), _bits(np.where(nan, 0, oc)))
