@@ -203,6 +203,7 @@ struct Scan2Shared {
     int inval[C::KB];
     int nxt[C::KB];        // next query of the batch with the same c* (KB = none)
     int ient[C::KB];       // log entry holding c*_j when the commit starts (-1 = none)
+    int vie[C::KB];        // vp_begin: log entry holding c*_j (64 = none)
     int freel[64];         // commit: free log entries, in lane order
     int asg[64];           // commit: log entry -> centroid position it now holds
     int slow_pos;
@@ -888,29 +889,30 @@ __device__ __forceinline__ void vp_begin(Scan2Shared<C>& sh, int qb, int off, in
     sh.vpos[lane] = lg_pos;
     sh.vfrom[lane] = 0;
     if (lane < C::KB) sh.vcs[lane] = st.cs;
-    wave_lds_sync();
-    // every lane against every pending query / log entry at once: the c* of
-    // the KB queries and the 64 entries' positions are LDS broadcasts, so no
-    // step waits for the previous one (the serial readlane / ballot chain
-    // this replaces kept wave 0 ~7k cycles behind the others at the A1 barrier)
+    // pairs (query, query with the same c*) and (log entry, query moving it) by
+    // position masks in LDS: qm[p] = the batch's queries whose c* is leaf p.
+    // dfs_inc is free here (the exact DFS runs in part 4, behind barriers) and
+    // only this wave touches it now; positions are unique among log entries
+    uint32_t* qm = reinterpret_cast<uint32_t*>(sh.dfs_inc);
     const int cs = st.cs;
-    int pred = -1, nxt = C::KB, first = C::KB, ie = 64;
-#pragma unroll
-    for (int k = 0; k < C::KB; ++k) {
-        const int ck = sh.vcs[k];  // -2 past the batch: matches no entry
-        const bool same = ck == cs;
-        pred = (k < lane && same) ? 64 + k : pred;               // last earlier query with the same c*
-        nxt = (k > lane && same && nxt == C::KB) ? k : nxt;      // first later one
-        first = (ck == lg_pos && first == C::KB) ? k : first;    // lane as log entry: first query moving it
-    }
-    if (lane < C::KB) {
-#pragma unroll
-        for (int e = 63; e >= 0; --e) ie = sh.vpos[e] == cs ? e : ie;  // lowest entry holding c*_j
-    }
-    st.pred = pred;
-    st.nxt = nxt;
-    st.first = first;
-    st.ie = ie;
+    const bool qv = lane < C::KB && cs >= 0;
+    if (qv) qm[cs] = 0u;
+    if (lg_pos >= 0) qm[lg_pos] = 0u;
+    if (lane < C::KB) sh.vie[lane] = 64;
+    wave_lds_sync();
+    if (qv) atomicOr(&qm[cs], 1u << lane);
+    wave_lds_sync();
+    const uint32_t mq = qv ? qm[cs] : 0u;               // queries sharing c*_j
+    const uint32_t me = lg_pos >= 0 ? qm[lg_pos] : 0u;  // queries moving entry e's centroid
+    const uint32_t below = lane < 32 ? (1u << lane) - 1u : ~0u;
+    const uint32_t above = lane < 31 ? ~((2u << lane) - 1u) : 0u;
+    const uint32_t mb = mq & below, ma = mq & above;
+    st.pred = mb ? 64 + (31 - __clz(mb)) : -1;   // last earlier query with the same c*
+    st.nxt = ma ? __ffs(ma) - 1 : C::KB;          // first later one
+    st.first = me ? __ffs(me) - 1 : C::KB;        // lane as log entry: first query moving it
+    for (uint32_t m = me; m; m &= m - 1u) atomicMin(&sh.vie[__ffs(m) - 1], lane);  // the entry holding c*_j
+    wave_lds_sync();
+    st.ie = lane < C::KB ? sh.vie[lane] : 64;
 }
 
 template <class C>
