@@ -22,7 +22,9 @@
 #include "gsc_device.h"
 
 extern "C" hipError_t gsc_launch_yakmo(int D, const gsc::ReduceFrame* frames, int nframes, const float* X, float* C,
-                                       float* fs, int* is, uint32_t* bits, int max_n, hipStream_t st);
+                                       float* fs, int* is, float* gsum, uint32_t* gbits, int max_n, hipStream_t st);
+extern "C" size_t gsc_yakmo_big_floats(int64_t total_points, int nframes);
+extern "C" size_t gsc_yakmo_big_words(int64_t total_points, int nframes);
 extern "C" hipError_t gsc_launch_ann_build(const float* pts, int n, int dd, int* pidx, int* cd, float* cv, float* lo,
                                            float* hi, float* bnd, float* val, hipStream_t st);
 extern "C" hipError_t gsc_launch_ann_query(const float* pts, int n, int dd, int* pidx, int* cd, float* cv, float* lo,
@@ -146,8 +148,8 @@ void yakmo_train_on_data(yakmo_t* ay, int* pointToCluster) {
     if (!ay) fatal(fn, "null handle");
     const int N = int(ay->rows), D = int(ay->cols), K = int(ay->k);
     if (!ay->supported) fatal(fn, "only yakmo_create(K,1,0,1,0,0,v) is implemented");
-    if (K <= 0 || K >= N || K > gsc::kMaxK || N > 262144 || !(D == 8 || D == 16 || D == 32))
-        fatal(fn, "unsupported shape (need 0 < K < N <= 262144, K <= 4096, D in {8, 16, 32})");
+    if (K <= 0 || K >= N || K > gsc::kMaxK || !(D == 8 || D == 16 || D == 32))
+        fatal(fn, "unsupported shape (need 0 < K < N, K <= 4096, D in {8, 16, 32})");
     if (!device_ok()) fatal(fn, "no gfx950 device (the MI355X hot path has no CPU fallback)");
     gsc::ReduceFrame fr{};
     fr.N = N;
@@ -155,12 +157,13 @@ void yakmo_train_on_data(yakmo_t* ay, int* pointToCluster) {
     fr.k_off = N;
     Dev<float> dX(ay->data.size()), dC(size_t(K) * D), dF(4 * size_t(N));
     Dev<int> dI(size_t(N) + K);
-    Dev<uint32_t> dB(size_t(N) / 32 + 4);
+    Dev<uint32_t> dB(gsc_yakmo_big_words(N, 1));
+    Dev<float> dS(gsc_yakmo_big_floats(N, 1));
     Dev<gsc::ReduceFrame> dFr(1);
-    if (!dX.p || !dC.p || !dF.p || !dI.p || !dB.p || !dFr.p) fatal(fn, "device allocation failed");
+    if (!dX.p || !dC.p || !dF.p || !dI.p || !dB.p || !dS.p || !dFr.p) fatal(fn, "device allocation failed");
     check(fn, hipMemcpy(dX.p, ay->data.data(), 4 * ay->data.size(), hipMemcpyHostToDevice));
     check(fn, hipMemcpy(dFr.p, &fr, sizeof(fr), hipMemcpyHostToDevice));
-    check(fn, gsc_launch_yakmo(D, dFr.p, 1, dX.p, dC.p, dF.p, dI.p, dB.p, N, nullptr));
+    check(fn, gsc_launch_yakmo(D, dFr.p, 1, dX.p, dC.p, dF.p, dI.p, dS.p, dB.p, N, nullptr));
     ay->centroids.resize(size_t(K) * D);
     ay->labels.resize(size_t(N));
     check(fn, hipMemcpy(ay->centroids.data(), dC.p, 4 * ay->centroids.size(), hipMemcpyDeviceToHost));

@@ -26,7 +26,10 @@
 #include "gsc_encoder.h"
 
 extern "C" hipError_t gsc_launch_yakmo(int D, const gsc::ReduceFrame* frames, int nframes, const float* X, float* C,
-                                       float* fs, int* is, uint32_t* bits, int max_n, hipStream_t st);
+                                       float* fs, int* is, float* gsum, uint32_t* gbits, int max_n, hipStream_t st);
+extern "C" size_t gsc_yakmo_big_floats(int64_t total_points, int nframes);
+extern "C" size_t gsc_yakmo_big_words(int64_t total_points, int nframes);
+extern "C" int gsc_yakmo_max_lds_points(void);
 extern "C" hipError_t gsc_launch_scan_pass(int D, gsc::ReduceFrame* frames, int nframes, int K, const float* X,
                                            float* C, int* is, float* fs, const float* rate_tab, double tol, int max_passes,
                                            int only_flagged, hipStream_t st);
@@ -288,8 +291,6 @@ int run_reduce_batch_dev(int D, int K, int precision, const std::vector<int>& Ns
     const int nf = int(Ns.size());
     if (nf == 0) return 0;
     if (D != 8 && D != 16 && D != 32) return fail("KNNScanReduce kernels support D = 8, 16 or 32 (ChunkSize 4, 8, 16)");
-    for (int n : Ns)
-        if (n > 262144) return fail("frame has more than 262144 chunks (yakmo seeding bitmap)");
     std::vector<ReduceFrame> fr(static_cast<size_t>(nf));
     int64_t no = 0, maxN = 0;
     for (int i = 0; i < nf; ++i) {
@@ -313,14 +314,17 @@ int run_reduce_batch_dev(int D, int K, int precision, const std::vector<int>& Ns
             fr[i].notify = notify + i;
         }
     }
-    DevBuf<float> dC, dF, dRate;
+    DevBuf<float> dC, dF, dRate, dYSum;
     DevBuf<int> dI;
     DevBuf<uint32_t> dBits;
     DevBuf<ReduceFrame> dFr;
     HIP_TRY(dC.alloc(size_t(nf) * K * D));
     HIP_TRY(dF.alloc(size_t(no) * 4));
     HIP_TRY(dI.alloc(size_t(no) + size_t(nf) * (size_t(K) + size_t(Kp))));
-    HIP_TRY(dBits.alloc(size_t(no / 32) + size_t(nf) * 2 + 2));
+    if (maxN > gsc_yakmo_max_lds_points()) {  // long frames: yakmo's bitmap and prefix summaries in HBM
+        HIP_TRY(dBits.alloc(gsc_yakmo_big_words(no, nf)));
+        HIP_TRY(dYSum.alloc(gsc_yakmo_big_floats(no, nf)));
+    }
     HIP_TRY(dFr.alloc(size_t(nf)));
     const std::vector<float> rt = rate_table(int(maxN));
     HIP_TRY(dRate.alloc(rt.size()));
@@ -331,7 +335,7 @@ int run_reduce_batch_dev(int D, int K, int precision, const std::vector<int>& Ns
     HIP_TRY(hipEventCreate(&e1));
     HIP_TRY(hipEventCreate(&e2));
     HIP_TRY(hipEventRecord(e0, nullptr));
-    HIP_TRY(gsc_launch_yakmo(D, dFr.p, nf, dX, dC.p, dF.p, dI.p, dBits.p, int(maxN), nullptr));
+    HIP_TRY(gsc_launch_yakmo(D, dFr.p, nf, dX, dC.p, dF.p, dI.p, dYSum.p, dBits.p, int(maxN), nullptr));
     HIP_TRY(hipEventRecord(e1, nullptr));
     HIP_TRY(launch_scan_passes(D, dFr.p, nf, K, dX, dC.p, dI.p, dF.p, dRate.p, precision));
     HIP_TRY(hipEventRecord(e2, nullptr));
@@ -1637,7 +1641,6 @@ int gsc_encode_wav_recon(const uint8_t* wav, size_t wav_len, const gsc_options* 
 int gsc_yakmo_seed_means(int n, int d, const float* x, int k, float* centroids) {
     if (ensure_device() != 0) return -1;
     if (k >= n || k <= 0 || k > kMaxK) return fail("yakmo needs 0 < k < n, k <= 4096");
-    if (n > 262144) return fail("yakmo seeding supports at most 262144 points");
     std::vector<float> X(x, x + size_t(n) * d), C;
     std::vector<int> cl, it, sl;
     // run only the seeding part: precision 0 => scan loop still runs once; use a
@@ -1648,7 +1651,7 @@ int gsc_yakmo_seed_means(int n, int d, const float* x, int k, float* centroids) 
     fr[0].N = n;
     fr[0].K = k;
     fr[0].k_off = n;
-    DevBuf<float> dX, dC, dF;
+    DevBuf<float> dX, dC, dF, dYSum;
     DevBuf<int> dI;
     DevBuf<uint32_t> dBits;
     DevBuf<ReduceFrame> dFr;
@@ -1656,11 +1659,12 @@ int gsc_yakmo_seed_means(int n, int d, const float* x, int k, float* centroids) 
     HIP_TRY(dC.alloc(size_t(k) * d));
     HIP_TRY(dF.alloc(size_t(n) * 4));
     HIP_TRY(dI.alloc(size_t(n) + size_t(k)));
-    HIP_TRY(dBits.alloc(size_t(n / 32) + 4));
+    HIP_TRY(dBits.alloc(gsc_yakmo_big_words(n, 1)));
+    HIP_TRY(dYSum.alloc(gsc_yakmo_big_floats(n, 1)));
     HIP_TRY(dFr.alloc(1));
     HIP_TRY(hipMemcpy(dX.p, X.data(), sizeof(float) * X.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(dFr.p, fr.data(), sizeof(ReduceFrame), hipMemcpyHostToDevice));
-    HIP_TRY(gsc_launch_yakmo(d, dFr.p, nf, dX.p, dC.p, dF.p, dI.p, dBits.p, n, nullptr));
+    HIP_TRY(gsc_launch_yakmo(d, dFr.p, nf, dX.p, dC.p, dF.p, dI.p, dYSum.p, dBits.p, n, nullptr));
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(centroids, dC.p, sizeof(float) * size_t(k) * d, hipMemcpyDeviceToHost));
     (void)C;

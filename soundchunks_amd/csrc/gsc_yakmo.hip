@@ -47,7 +47,8 @@ constexpr int kYThreads = 768;
 __device__ __forceinline__ bool yakmo_idle_wave(int w) { return w == 4 || w == 8 || w == 11; }
 // distance thread index of a distance wave's lane
 __device__ __forceinline__ int yakmo_dist_index(int w, int lane) { return (w - 1 - w / 4) * 64 + lane; }
-constexpr int kYBits = 262144 / 32;   // chosen-point bitmap in LDS (N <= 262144)
+constexpr int kYMaxLds = 262144;      // frames up to this many points keep the yakmo state in LDS
+constexpr int kYBits = kYMaxLds / 32;  // chosen-point bitmap in LDS
 constexpr int kYPre = 3;              // d0 / seed-id prefetch depth (steps); X rows: 1
 
 #ifdef GSC_STAMPS
@@ -360,10 +361,16 @@ __device__ int pick_lower_bound(float target, float total, int N, const float* c
 // dynamic LDS bytes of a frame with N points
 __host__ __device__ constexpr size_t yakmo_dyn_lds(int N) { return size_t(3) * size_t((N + 63) / 64) * sizeof(float); }
 
-template <int D>
+// BIG: frames of more than kYMaxLds points (long -fl frames at small ChunkSize)
+// keep the chosen-point bitmap and the per-block prefix summaries in HBM
+// (gbits / gsum, frame slices at (n_off >> 5) + fi words and 3 ((n_off >> 6) +
+// fi) floats) instead of LDS; one workgroup's own stores and loads, ordered by
+// program order and the pick-end barrier (L1 is per CU and write-through)
+template <int D, bool BIG>
 __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFrame* __restrict__ frames, int nframes,
                                                                  const float* __restrict__ Xall, float* __restrict__ Call,
-                                                                 float* __restrict__ f_scratch, int* __restrict__ i_scratch) {
+                                                                 float* __restrict__ f_scratch, int* __restrict__ i_scratch,
+                                                                 float* __restrict__ gsum, uint32_t* __restrict__ gbits) {
     __shared__ YakmoShared sh;
     extern __shared__ __attribute__((aligned(16))) float ydyn[];
     const int fi = blockIdx.x;
@@ -371,9 +378,12 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
     const ReduceFrame fr = frames[fi];
     const int N = fr.N, K = fr.K;
     const int nb = (N + 63) >> 6;
-    float* ck = ydyn;
-    float* bmn = ydyn + nb;
-    float* bmx = ydyn + 2 * nb;
+    float* const sum0 = BIG ? gsum + 3 * ((fr.n_off >> 6) + fi) : ydyn;
+    float* ck = sum0;
+    float* bmn = sum0 + nb;
+    float* bmx = sum0 + 2 * nb;
+    uint32_t* const chosen = BIG ? gbits + (fr.n_off >> 5) + fi : sh.chosen;
+    const int nchosen = BIG ? (N + 31) >> 5 : kYBits;
     const float* __restrict__ X = Xall + fr.x_off;
     float* C = Call + fr.c_off;
     float* d0 = f_scratch + fr.n_off * 4;
@@ -393,7 +403,7 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
         norm[n] = s;
         xm = fmaxf(xm, __builtin_isnan(s) ? 3.4028235e38f : s);
     }
-    for (int w = tid; w < kYBits; w += kYThreads) sh.chosen[w] = 0u;
+    for (int w = tid; w < nchosen; w += kYThreads) chosen[w] = 0u;
     if (tid == 0) sh.xmax = 0.0f;
     __syncthreads();
     atomicMax(reinterpret_cast<unsigned*>(&sh.xmax), __float_as_uint(xm));  // non-negative floats order as integers
@@ -440,11 +450,11 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
                 idx = (uint32_t)(int64_t)(float)pick_lower_bound(fm(r, total), total, N, ck, bmn, bmx, d0, lane);
             }
             // collision walk (@0x180001b20) and clamp (@0x180001c50)
-            while (idx < (uint32_t)N && ((sh.chosen[idx >> 5] >> (idx & 31)) & 1u))
+            while (idx < (uint32_t)N && ((chosen[idx >> 5] >> (idx & 31)) & 1u))
                 idx = (idx < (uint32_t)(N - 1)) ? idx + 1 : 0u;
             if (idx >= (uint32_t)N) idx = (uint32_t)(N - 1);
             if (lane == 0) {
-                sh.chosen[idx >> 5] |= 1u << (idx & 31);
+                chosen[idx >> 5] |= 1u << (idx & 31);
                 const float cn = norm[idx];
                 sh.cn = cn;
                 sh.cmax = i == 0 ? cn : fmaxf(sh.cmax, cn);
@@ -654,24 +664,40 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
 
 using namespace gsc;
 
+// gsum / gbits: HBM state of frames over kYMaxLds points (see yakmo_seed2_kernel;
+// gsc_yakmo_big_floats / _words give the sizes); unused otherwise
 extern "C" hipError_t gsc_launch_yakmo(int D, const ReduceFrame* frames, int nframes, const float* X, float* C,
-                                       float* fs, int* is, uint32_t* /*bits*/, int max_n, hipStream_t st) {
+                                       float* fs, int* is, float* gsum, uint32_t* gbits, int max_n, hipStream_t st) {
     dim3 grid(nframes), block(kYThreads);
-    const size_t shm = yakmo_dyn_lds(max_n);
+    const bool big = max_n > kYMaxLds;
+    if (big && (!gsum || !gbits)) return hipErrorInvalidValue;
+    const size_t shm = big ? 0 : yakmo_dyn_lds(max_n);
     hipError_t e = hipSuccess;
     switch (D) {
-#define YK(DV)                                                                                                  \
-    case DV:                                                                                                    \
-        e = hipFuncSetAttribute((const void*)yakmo_seed2_kernel<DV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                (int)shm);                                                                      \
-        if (e != hipSuccess) return e;                                                                          \
-        hipLaunchKernelGGL(yakmo_seed2_kernel<DV>, grid, block, shm, st, frames, nframes, X, C, fs, is);         \
+#define YK(DV, B)                                                                                                 \
+    e = hipFuncSetAttribute((const void*)yakmo_seed2_kernel<DV, B>, hipFuncAttributeMaxDynamicSharedMemorySize,    \
+                            (int)shm);                                                                            \
+    if (e != hipSuccess) return e;                                                                                \
+    hipLaunchKernelGGL((yakmo_seed2_kernel<DV, B>), grid, block, shm, st, frames, nframes, X, C, fs, is, gsum, gbits);
+    case 8:
+        if (big) { YK(8, true) } else { YK(8, false) }
         break;
-        YK(8)
-        YK(16)
-        YK(32)
+    case 16:
+        if (big) { YK(16, true) } else { YK(16, false) }
+        break;
+    case 32:
+        if (big) { YK(32, true) } else { YK(32, false) }
+        break;
 #undef YK
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
+
+// HBM state of frames over kYMaxLds points: prefix summaries (floats) and chosen bitmaps (words)
+// for nframes frames of total_points points
+extern "C" size_t gsc_yakmo_big_floats(int64_t total_points, int nframes) {
+    return size_t(3) * size_t(total_points / 64 + nframes + 1);
+}
+extern "C" size_t gsc_yakmo_big_words(int64_t total_points, int nframes) { return size_t(total_points / 32 + nframes + 1); }
+extern "C" int gsc_yakmo_max_lds_points(void) { return kYMaxLds; }

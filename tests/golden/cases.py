@@ -88,6 +88,9 @@ CASES = {
     # cost loop (encoder.lpr:1337-1351) -- K = 485 and 1852 here, not powers of two
     "syn8s_br128_vfr05_cs8": (lambda: _synth(8.0), ["-br128", "-vfr0.5", "-cs8"]),
     "syn8s_br128_vfr05_cs16": (lambda: _synth(8.0), ["-br128", "-vfr0.5", "-cs16"]),
+    # a frame of more than 262,144 chunks (13-s frames at 48 kHz stereo -cs4: N ~ 312,000): yakmo's
+    # chosen-point bitmap and prefix summaries live in HBM instead of LDS
+    "syn13s_48k_cs4_cpf256_fl13000": (lambda: _synth(13.0, 48000), ["-cs4", "-cpf256", "-fl13000"]),
 }
 
 

@@ -104,7 +104,9 @@ def _yakmo_dataset(kind, n, d, seed):
 
 
 @pytest.mark.parametrize("kind,n,d,k", [("gauss", 5000, 16, 256), ("integer", 3000, 16, 512),
-                                        ("outliers", 7000, 8, 256), ("gauss", 20000, 16, 1024)])
+                                        ("outliers", 7000, 8, 256), ("gauss", 20000, 16, 1024),
+                                        # more than 262,144 points: bitmap and prefix summaries in HBM
+                                        ("gauss", 300000, 8, 256), ("integer", 270000, 16, 256)])
 def test_yakmo_seed_means_synthetic(oracle, kind, n, d, k):
     """The binade-exact prefix fast path (gsc_yakmo.hip) against the oracle's sequential f32 chain."""
     import ctypes
