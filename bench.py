@@ -229,10 +229,13 @@ def main():
             st, en = broadcast_bounds(st, en, device=dev)
         b, e = bounds_range(st, en, cs, ch, rank, ws)
         info["frames"], info["range"] = len(st), (b, e)
+        t_enc = time.perf_counter()
         if rank == 0:
             out = p.encode(b, e)
         else:
             out = enc.prepare_frames(wav, st, en, b, e).encode(b, e)
+        if os.environ.get("BENCH_STEP_TIMING"):  # diagnostic: the encode call inside the step
+            print(f"step: encode call {(time.perf_counter() - t_enc) * 1e3:.1f} ms", file=sys.stderr, flush=True)
         if dist is not None:
             out = gather_streams(out, device=dev)
         return out, nxt
@@ -252,8 +255,11 @@ def main():
     fut = pool.submit(prepare_job) if rank == 0 else None
     timings = []
     for k in range(args.steps):
+        t_step = time.perf_counter()
         _, fut = step(fut, k + 1 < args.steps)
         timings.append(sc.Encoder.last_timing())
+        if os.environ.get("BENCH_STEP_TIMING"):
+            print(f"step: {(time.perf_counter() - t_step) * 1e3:.1f} ms", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()

@@ -139,16 +139,26 @@ int ensure_device() {
     return 0;
 }
 
+// diagnostic (GSC_HOST_TIMING): host time inside hipMalloc / hipFree of DevBufs
+std::atomic<int64_t> g_devbuf_ns{0};
+
 template <typename T>
 struct DevBuf {
     T* p = nullptr;
     size_t n = 0;
     ~DevBuf() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            const double t = now_ms();
+            (void)hipFree(p);
+            g_devbuf_ns.fetch_add(int64_t((now_ms() - t) * 1e6));
+        }
     }
     hipError_t alloc(size_t count) {
         n = count;
-        return hipMalloc(&p, sizeof(T) * std::max<size_t>(count, 1));
+        const double t = now_ms();
+        const hipError_t e = hipMalloc(&p, sizeof(T) * std::max<size_t>(count, 1));
+        g_devbuf_ns.fetch_add(int64_t((now_ms() - t) * 1e6));
+        return e;
     }
 };
 
@@ -1280,8 +1290,10 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
     if (std::getenv("GSC_HOST_TIMING"))
         std::fprintf(stderr,
                      "host timing [ms]: frames+dsp %.1f (dsp %.1f) | reduce (yakmo %.1f scan %.1f) %.1f |"
-                     " post after the scan %.1f (in the scan tail %.1f, KNNFit kernels %.1f, %d groups) | concat %.1f\n",
-                     t1 - t0, dsp_ms, yak_ms, scan_ms, t2 - t1, t3 - t2, overlap_ms, pc.knn_ms, pc.groups, t4 - t3);
+                     " post after the scan %.1f (in the scan tail %.1f, KNNFit kernels %.1f, %d groups) | concat %.1f"
+                     " | hipMalloc/hipFree so far %.1f\n",
+                     t1 - t0, dsp_ms, yak_ms, scan_ms, t2 - t1, t3 - t2, overlap_ms, pc.knn_ms, pc.groups, t4 - t3,
+                     double(g_devbuf_ns.exchange(0)) / 1e6);
     if (std::getenv("GSC_HOST_TIMING") && !red_idx.empty()) {  // per-frame pass counts (scan tail)
         std::vector<int> h(kMaxScanIters + 1, 0);
         for (int i : red_idx) h[std::min(kMaxScanIters, std::max(0, frames[i].scan_iters))]++;
