@@ -22,6 +22,12 @@ file); --strong keeps one --seconds file for any world size.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--seconds S]
                   [--config c1|c2|c3|c4|c5|c5cs4|br128] [--strong] [--no-cpu-baseline]
+                  [--backend nccl|gloo]
+
+After the timed loop the last step's output is checked frame by frame against
+the oracle's SHA-256 digests of the same workload (tests/golden/
+bench_digests.json; c4: corpus_meta.json): "bit_exact" in the line, and a
+mismatch exits with status 3.
 
 --gpus N without a launcher's WORLD_SIZE spawns N worker processes (one per
 GPU, RANK/LOCAL_RANK/WORLD_SIZE, rendezvous at 127.0.0.1) before any GPU call.
@@ -58,6 +64,8 @@ CORPUS = ROOT / "tests" / "golden" / "lame_test"
 VALU_F32_PEAK_TOPS = 78.6  # non-fused f32 VALU ops/s: half the 157.3 TFLOPS FMA-counted peak
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md (spec)
 PMC_SUMMARY = ROOT / "profiles" / "r03" / "pmc_summary.json"  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
+DIGESTS = ROOT / "tests" / "golden" / "bench_digests.json"  # oracle per-frame .gsc digests (make_bench_digests.py)
+CORPUS_META = ROOT / "tests" / "golden" / "corpus_meta.json"  # oracle .gsc digests of the lame_test files
 
 
 def _dist_env():
@@ -73,6 +81,25 @@ def _cpu_model() -> str:
     except OSError:
         pass
     return "unknown"
+
+
+def _cpu_share() -> tuple[int, int, int | None]:
+    """(threads to use, CPUs in the affinity mask, CPUs of the cgroup quota or
+    None).  The GPU box's affinity mask lists every CPU of the host, but its
+    cgroup (cpu.max) grants this job a quota (16 CPUs per GPU): more threads
+    than the quota only time-slice the same CPU share."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return (min(aff, quota) if quota else aff), aff, quota
 
 
 def cpu_baseline(cfg: str, argv, rate: int, channels: int, frame_seconds: float, threads: int,
@@ -120,31 +147,66 @@ def cpu_baseline(cfg: str, argv, rate: int, channels: int, frame_seconds: float,
     for t in ths:
         t.join()
     w1 = statistics.median(walls)
-    t = time.perf_counter()
-    if len(sample) == 1:
-        oracle_ffi.encode(sample[0], argv, threads=threads)
-    else:  # corpus files side by side, one encode per thread slot
-        from concurrent.futures import ThreadPoolExecutor as TP
+    wns = []
+    for _ in range(runs):
+        t = time.perf_counter()
+        if len(sample) == 1:
+            oracle_ffi.encode(sample[0], argv, threads=threads)
+        else:  # corpus files side by side, one encode per thread slot
+            from concurrent.futures import ThreadPoolExecutor as TP
 
-        with TP(threads) as pool:
-            list(pool.map(lambda w: oracle_ffi.encode(w, argv, threads=1), sample))
-    wn = time.perf_counter() - t
+            with TP(threads) as pool:
+                list(pool.map(lambda w: oracle_ffi.encode(w, argv, threads=1), sample))
+        wns.append(time.perf_counter() - t)
+    wn = statistics.median(wns)
     nsamp = sum((len(w) - 44) // 2 for w in sample)
     allv = nsamp / wn / 1e6
-    try:
-        share = len(os.sched_getaffinity(0))
-    except AttributeError:
-        share = os.cpu_count()
+    _, share, quota = _cpu_share()
     what = (f"{len(sample)} corpus files ({nsamp / rate:.1f} s)" if cfg == "c4"
             else f"{threads} full {frame_seconds:g}-s frames ({frame_seconds * threads:g} s) of the same synthetic "
                  f"{rate} Hz {channels}-ch signal and flags")
     return {"value": round(allv, 6), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"all-core: {what}, oracle/ C restatement frame-parallel on {threads} threads, 1 run "
-                      f"({wn:.1f} s); single-thread: one full frame, median of {runs} side-by-side runs",
+            "sample": f"all-core: {what}, oracle/ C restatement frame-parallel on {threads} threads, median of "
+                      f"{runs} runs ({', '.join(f'{w:.1f}' for w in wns)} s); single-thread: one full frame, median "
+                      f"of {runs} side-by-side runs",
             "single_thread": {"value": round(one_samples / w1 / 1e6, 6), "cores": 1, "wall_s": round(w1, 2),
                               "runs_s": [round(w, 2) for w in walls]},
-            "all_core": {"value": round(allv, 6), "cores": threads, "wall_s": round(wn, 2)},
-            "cpu_model": _cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": share}
+            "all_core": {"value": round(allv, 6), "cores": threads, "wall_s": round(wn, 2),
+                         "runs_s": [round(w, 2) for w in wns]},
+            "cpu_model": _cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": share, "cgroup_cpus": quota,
+            "cores_note": "threads = the CPUs this job may use: the cgroup cpu.max quota when one is set (the GPU "
+                          "box grants 16 CPUs per GPU while its affinity mask lists every host CPU), else the "
+                          "affinity mask"}
+
+
+def frame_digest_check(key: str, frame_begin: int, blob: bytes, sizes, frames_total: int) -> tuple[int, int, int]:
+    """This rank's frames against the oracle's per-frame SHA-256 digests of the
+    same workload (tests/golden/bench_digests.json; data only -- the oracle
+    itself is not run here): (frames checked, frames differing, frames with a
+    digest).  A .gsc is its frames' SaveStream bytes in order
+    (encoder.lpr:1181-1215), so the per-frame split of the encoder's own
+    output is exact."""
+    import hashlib
+
+    if not DIGESTS.exists():
+        return 0, 0, 0
+    ent = json.loads(DIGESTS.read_text()).get(key)
+    if ent is None:
+        return 0, 0, 0
+    if int(ent["frames"]) != frames_total:
+        return 1, 1, len(ent["per_frame"])  # a different frame cut is a mismatch
+    want = ent["per_frame"]
+    checked = bad = 0
+    o = 0
+    for i, n in enumerate(sizes):
+        h = want.get(str(frame_begin + i))
+        if h is not None:
+            checked += 1
+            bad += hashlib.sha256(blob[o:o + n]).hexdigest() != h
+        o += n
+    if o != len(blob):
+        bad += 1
+    return checked, bad, len(want)
 
 
 def oracle_ffi_first_frame_wav(wav: bytes, argv) -> bytes:
@@ -168,10 +230,15 @@ def main():
                     help="audio seconds per GPU (weak) or in total (--strong); 1024 s = 256 frames of 4 s")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--strong", action="store_true", help="one fixed-length file for any world size")
-    ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="all-core CPU baseline threads (the GPU box's CPU share is 16 per GPU)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="all-core CPU baseline threads (default: the job's CPU share, cgroup quota or affinity)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo rehearses the "
+                         "multi-rank path on host tensors, e.g. 2 ranks on a one-GPU box)")
     args = ap.parse_args()
+    if args.cpu_threads <= 0:
+        args.cpu_threads = _cpu_share()[0]
 
     ws, rank, local = _dist_env()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -186,23 +253,27 @@ def main():
     import torch
 
     dist = None
-    dev = torch.device("cuda", local)
+    # one process per GPU; with more ranks than visible GPUs (the gloo rehearsal
+    # on a one-GPU box) ranks share devices round-robin
+    gpu = local % max(1, torch.cuda.device_count())
+    dev = torch.device("cuda", gpu)
+    cdev = dev if args.backend == "nccl" else torch.device("cpu")  # where the collectives' tensors live
     if ws > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(gpu)
+        dist.init_process_group(args.backend)
     import soundchunks_amd as sc
     from soundchunks_amd.shard import bounds_range, broadcast_bounds, gather_streams
     from soundchunks_amd.synth import synth_wav
 
     if ws > 1:
-        sc.set_device(local)
+        sc.set_device(gpu)
 
     argv, ch, rate, cs, desc = CONFIGS[args.config]
     enc = sc.Encoder(argv)
     if args.config == "c4":
-        return bench_corpus(args, enc, argv, desc, ws, rank, local, dist)
+        return bench_corpus(args, enc, argv, desc, ws, rank, cdev, dist)
     total_seconds = args.seconds if args.strong else args.seconds * ws
     wav = synth_wav(total_seconds, rate, ch)  # the job's input, in host memory on every rank
 
@@ -226,18 +297,19 @@ def main():
             if prefetch:
                 nxt = pool.submit(prepare_job)
         if dist is not None:  # rank 0's PrepareFrames boundaries to every rank
-            st, en = broadcast_bounds(st, en, device=dev)
+            st, en = broadcast_bounds(st, en, device=cdev)
         b, e = bounds_range(st, en, cs, ch, rank, ws)
         info["frames"], info["range"] = len(st), (b, e)
         t_enc = time.perf_counter()
         if rank == 0:
-            out = p.encode(b, e)
+            out, sizes = p.encode_frames(b, e)
         else:
-            out = enc.prepare_frames(wav, st, en, b, e).encode(b, e)
+            out, sizes = enc.prepare_frames(wav, st, en, b, e).encode_frames(b, e)
+        info["own"] = (b, out, sizes)
         if os.environ.get("BENCH_STEP_TIMING"):  # diagnostic: the encode call inside the step
             print(f"step: encode call {(time.perf_counter() - t_enc) * 1e3:.1f} ms", file=sys.stderr, flush=True)
         if dist is not None:
-            out = gather_streams(out, device=dev)
+            out = gather_streams(out, device=cdev)
         return out, nxt
 
     # warmup (untimed): the first one, run alone, is the single-job latency
@@ -254,9 +326,10 @@ def main():
     t0 = time.perf_counter()
     fut = pool.submit(prepare_job) if rank == 0 else None
     timings = []
+    whole = None
     for k in range(args.steps):
         t_step = time.perf_counter()
-        _, fut = step(fut, k + 1 < args.steps)
+        whole, fut = step(fut, k + 1 < args.steps)
         timings.append(sc.Encoder.last_timing())
         if os.environ.get("BENCH_STEP_TIMING"):
             print(f"step: {(time.perf_counter() - t_step) * 1e3:.1f} ms", file=sys.stderr, flush=True)
@@ -265,12 +338,28 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([dt], device=dev)
+        t = torch.tensor([dt], device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    # bit-exactness of the last timed step's output (after the clock stopped):
+    # every rank checks its own frames against the oracle digests, rank 0 also
+    # the length of the gathered file when every frame has a digest
+    key = f"{args.config}:{total_seconds:g}"
+    fb, blob, sizes = info["own"]
+    checked, bad, listed = frame_digest_check(key, fb, blob, sizes, info["frames"])
+    if dist is not None:
+        t = torch.tensor([checked, bad], dtype=torch.int64, device=cdev)
+        dist.all_reduce(t)
+        checked, bad = (int(v) for v in t.tolist())
     if rank != 0:
         dist.destroy_process_group()
+        if bad:
+            sys.exit(3)
         return
+    if listed == info["frames"] and checked == listed:
+        want_len = json.loads(DIGESTS.read_text())[key].get("total_bytes")
+        if want_len is not None and len(whole) != int(want_len):
+            bad += 1
     n_samples = int(round(total_seconds * rate)) * ch
     value = n_samples * args.steps / dt / 1e6
     result = base_result(args, ws, dt, value, desc, enc, timings[-1], cs, argv, rate, ch)
@@ -281,12 +370,21 @@ def main():
     result["prepare_ms"] = round(info["prepare_ms"], 1)
     result["job_latency_ms"] = None if lat is None else round(lat, 1)
     result["realtime_x"] = round(value / (rate * ch / 1e6), 2)
+    result["bit_exact"] = (bad == 0) if checked else None
+    result["bit_exact_check"] = {
+        "digests": f"tests/golden/bench_digests.json[{key}] (oracle SaveStream bytes per frame)",
+        "frames_checked": checked, "frames_differing": bad, "frames_total": info["frames"],
+        "whole_file": checked == info["frames"],
+        "note": None if checked else "no oracle digests for this workload: not checked"}
     if not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.config, argv, rate, ch, enc.frame_length / 1000.0,
                                               args.cpu_threads)
     print(json.dumps(result))
     if dist is not None:
         dist.destroy_process_group()
+    if bad:
+        print(f"bench.py: {bad} frame(s) differ from the oracle digests", file=sys.stderr)
+        sys.exit(3)
 
 
 def base_result(args, ws, dt, value, desc, enc, tm, cs, argv, rate, ch) -> dict:
@@ -348,7 +446,7 @@ def base_result(args, ws, dt, value, desc, enc, tm, cs, argv, rate, ch) -> dict:
     }
 
 
-def bench_corpus(args, enc, argv, desc, ws, rank, local, dist):
+def bench_corpus(args, enc, argv, desc, ws, rank, cdev, dist):
     """configs[3]: the 22-file lame_test corpus as ONE batch -- every frame of
     every file in one device launch per stage (gsc_encode_many), frames of the
     batch sharded across ranks by chunk count, one .gsc per file on rank 0."""
@@ -358,10 +456,9 @@ def bench_corpus(args, enc, argv, desc, ws, rank, local, dist):
 
     names = sorted(n for n in os.listdir(CORPUS) if n.endswith(".wav"))
     wavs = [(CORPUS / n).read_bytes() for n in names]
-    dev = torch.device("cuda", local)
 
     def step():
-        return sc.encode_many(wavs, argv, rank=rank, world_size=ws, device=dev if dist is not None else None)
+        return sc.encode_many(wavs, argv, rank=rank, world_size=ws, device=cdev if dist is not None else None)
 
     lat = None
     for w in range(args.warmup):
@@ -382,7 +479,7 @@ def bench_corpus(args, enc, argv, desc, ws, rank, local, dist):
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([dt], device=dev)
+        t = torch.tensor([dt], device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     if rank != 0:
@@ -398,11 +495,24 @@ def bench_corpus(args, enc, argv, desc, ws, rank, local, dist):
     result["job_latency_ms"] = None if lat is None else round(lat, 1)
     result["realtime_x"] = round(value / (44100 / 1e6), 2)
     result["outputs_bytes"] = sum(len(o) for o in outs)
+    # every file's .gsc of the last timed step against the oracle's digest (corpus_meta.json)
+    import hashlib
+
+    meta = json.loads(CORPUS_META.read_text())
+    bad = sum(hashlib.sha256(o).hexdigest() != meta["files"][n]["gsc_sha256"] for n, o in zip(names, outs))
+    if meta["argv"] != list(argv):
+        bad = len(names)
+    result["bit_exact"] = bad == 0
+    result["bit_exact_check"] = {"digests": "tests/golden/corpus_meta.json (oracle .gsc per file)",
+                                 "files_checked": len(names), "files_differing": bad, "whole_file": True}
     if not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline("c4", argv, 44100, 1, enc.frame_length / 1000.0, args.cpu_threads)
     print(json.dumps(result))
     if dist is not None:
         dist.destroy_process_group()
+    if bad:
+        print(f"bench.py: {bad} corpus file(s) differ from the oracle digests", file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -117,6 +117,14 @@ gsc_prepared *gsc_prepare(const uint8_t *wav, size_t wav_len, const gsc_options 
 int gsc_prepared_frame_count(const gsc_prepared *p);
 int gsc_prepared_frame_chunks(const gsc_prepared *p, int *chunks);
 int gsc_encode_prepared(gsc_prepared *p, int frame_begin, int frame_end, uint8_t **out, size_t *out_len);
+/* gsc_encode_prepared, plus each frame's share of the returned bytes
+ * (frame_bytes[i - frame_begin], frame_end - frame_begin entries): a .gsc is
+ * the concatenation of its frames' TFrame.SaveStream bytes
+ * (encoder.lpr:980-1107, 1181-1215), so the caller can split it per frame
+ * (bench.py's per-frame bit-exactness digests).  Every prepared entry point
+ * refuses frames outside the range a gsc_prepare_frames handle loaded. */
+int gsc_encode_prepared_frames(gsc_prepared *p, int frame_begin, int frame_end, uint8_t **out, size_t *out_len,
+                               size_t *frame_bytes);
 double gsc_prepared_prepare_ms(const gsc_prepared *p);
 /* The frame boundaries PrepareFrames chose: sample index of every frame's
  * first and last sample (gsc_prepared_frame_count entries each). */
@@ -135,7 +143,8 @@ void gsc_prepared_free(gsc_prepared *p);
  * file gets its own Load + PrepareFrames, then the frames of ALL files form
  * one frame list, so every stage runs one device launch for the whole batch.
  * The files must share channel count, sample rate and the resulting
- * ChunksPerFrame.  gsc_prepared_file_frames writes file_count + 1 entries: the
+ * ChunksPerFrame.  A gsc_prepare / gsc_prepare_frames handle is one file
+ * (file_count 1).  gsc_prepared_file_frames writes file_count + 1 entries: the
  * first frame of every file, then the total.  gsc_encode_prepared_files
  * encodes frames [frame_begin, frame_end) of the list and also writes, per
  * file, how many of the returned bytes belong to it (files in order; a file's

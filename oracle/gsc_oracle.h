@@ -47,7 +47,9 @@ void ora_default_params(gsc_params *p);
 /* argv-style option parsing, same prefix semantics as encoder.lpr:201-227 */
 void ora_parse_params(gsc_params *p, int argc, const char *const *argv);
 
-/* Full encode.  Returns 0 on success; *out is malloc'd (free with ora_free).
+/* Full encode.  Returns 0 on success, -4 when a frame fails SaveStream's
+ * Assert(reducedChunks.Count <= 4096) (encoder.lpr:986; -pr0 passthrough
+ * frames); *out is malloc'd (free with ora_free).
  * threads <= 0 => 1.  Frames are independent; the result does not depend on
  * the thread count. */
 int ora_encode(const uint8_t *wav, size_t wav_len, const gsc_params *p, int threads, uint8_t **out,
@@ -66,6 +68,10 @@ int ora_encode_recon(const uint8_t *wav, size_t wav_len, const gsc_params *p, in
  * SaveStream bytes; *frame_count (may be NULL) = frames in the file. */
 int ora_encode_frames(const uint8_t *wav, size_t wav_len, const gsc_params *p, int frame_begin, int frame_end,
                       int threads, uint8_t **out, size_t *out_len, int *frame_count);
+/* The listed frames (distinct indices), concatenated in list order, with each
+ * one's byte count in frame_bytes[k]. */
+int ora_encode_frame_list(const uint8_t *wav, size_t wav_len, const gsc_params *p, const int *frames, int nframes,
+                          int threads, uint8_t **out, size_t *out_len, size_t *frame_bytes, int *frame_count);
 
 /* Statistics of the last ora_encode (process-global, for tests/bench). */
 typedef struct {

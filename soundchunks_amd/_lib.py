@@ -105,6 +105,8 @@ SIGNATURES = {
                                                  ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]),
     "gsc_encode_prepared": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_U8P),
                                            ctypes.POINTER(ctypes.c_size_t)]),
+    "gsc_encode_prepared_frames": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_U8P),
+                                                  ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]),
     "gsc_prepared_prepare_ms": (ctypes.c_double, [ctypes.c_void_p]),
     "gsc_prepared_free": (None, [ctypes.c_void_p]),
     "gsc_frame_dsp": (ctypes.c_int, [_U8P, ctypes.c_size_t, ctypes.POINTER(GscOptions), ctypes.c_int, _IP,

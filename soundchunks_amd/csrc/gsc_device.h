@@ -80,7 +80,7 @@ struct PackFrame {
     int64_t out_off;      // N ints: KNNFit best (4c + 2neg + rev) at best + out_off
     int64_t r_off;        // R ints: use counts (out) / old -> new index map (in) at + r_off
     int64_t w_off;        // bitstream: pack_word_capacity(N) zeroed u32 words at words + w_off
-    int32_t N, R;         // chunkRefs count, reducedChunks count before pruning (<= kMaxK)
+    int32_t N, R;         // chunkRefs count, reducedChunks count before pruning (-pr0 passthrough: N)
     int32_t nbits;        // out: bits of the stream (16-bit words written = ceil(nbits / 16))
     int32_t pad_;
 };

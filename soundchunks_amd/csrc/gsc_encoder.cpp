@@ -300,6 +300,7 @@ int Encoder::plan(std::string* err) {
     // the cut: cur += pw[i]; at block-aligned i with cur >= perFramePower a frame
     // ends at i - 1 and cur restarts at 0 (pw[i] itself is not carried over)
     cut_frames(P, per_frame);
+    file_first_ = {0, int(fr_start_.size())};  // one file
     if (tm)
         std::fprintf(stderr,
                      "plan [ms]: avg %.1f pw+total %.1f cut %.1f | exact sums: avg %lld/%lld blocks on the grid "
@@ -469,13 +470,17 @@ int Encoder::prepare_bounds(const uint8_t* wav, size_t len, const int* starts, c
         *err = "frame bounds do not cover the file";
         return -1;
     }
+    // frame 0 may be empty, (0, -1): the reference's cut ends it at i = 0 when
+    // curPower >= perFramePower there (encoder.lpr:1411-1417; cut_frames keeps it)
     for (int i = 0; i < nframes; ++i)
-        if (ends[i] < starts[i] || (i > 0 && starts[i] != ends[i - 1] + 1) || starts[i] % block_ != 0) {
+        if (ends[i] < starts[i] - (i == 0 ? 1 : 0) || (i > 0 && starts[i] != ends[i - 1] + 1) ||
+            starts[i] % block_ != 0) {
             *err = "frame bounds are not contiguous block-aligned frames";
             return -1;
         }
     fr_start_.assign(starts, starts + nframes);
     fr_end_.assign(ends, ends + nframes);
+    file_first_ = {0, nframes};
     if (e > b) rc = load(wav, len, starts[b], int64_t(ends[e - 1]) + 1, err);
     return rc;
 }

@@ -38,15 +38,26 @@ __global__ __launch_bounds__(1024) void usecount_kernel(const PackFrame* __restr
     __shared__ int h[kMaxK];
     const PackFrame& f = frames[blockIdx.x];
     const int N = f.N, R = f.R;
+    const int* b = best + f.out_off;
+    int* c = counts + f.r_off;
+    if (R > kMaxK) {
+        // -pr0 passthrough frames: reducedChunks = every chunk (encoder.lpr:891-905),
+        // more entries than the LDS histogram holds; count in the frame's slab
+        for (int i = threadIdx.x; i < R; i += blockDim.x) c[i] = 0;
+        __syncthreads();
+        for (int j = threadIdx.x; j < N; j += blockDim.x) {
+            const int v = b[j];
+            if (v >= 0) atomicAdd(&c[v >> 2], 1);
+        }
+        return;
+    }
     for (int i = threadIdx.x; i < R; i += blockDim.x) h[i] = 0;
     __syncthreads();
-    const int* b = best + f.out_off;
     for (int j = threadIdx.x; j < N; j += blockDim.x) {
         const int v = b[j];
         if (v >= 0) atomicAdd(&h[v >> 2], 1);  // -1: a tie-overflow query awaiting the ANN replay
     }
     __syncthreads();
-    int* c = counts + f.r_off;
     for (int i = threadIdx.x; i < R; i += blockDim.x) c[i] = h[i];
 }
 

@@ -511,7 +511,15 @@ int run_knnfit_overflow(int CS, const std::vector<FitFrame>& fr, const std::vect
     }
     HIP_TRY(hipMemcpyAsync(dTrees.p, trees.data(), sizeof(AnnTree) * size_t(nt), hipMemcpyHostToDevice, st));
     const bool timing = std::getenv("GSC_HOST_TIMING") != nullptr;
-    hipEvent_t eb0 = nullptr, eb1 = nullptr;
+    struct EvPair {  // diagnostic events, released on every return path
+        hipEvent_t a = nullptr, b = nullptr;
+        ~EvPair() {
+            if (a) (void)hipEventDestroy(a);
+            if (b) (void)hipEventDestroy(b);
+        }
+    } ev;
+    hipEvent_t& eb0 = ev.a;
+    hipEvent_t& eb1 = ev.b;
     if (timing) {
         HIP_TRY(hipEventCreate(&eb0));
         HIP_TRY(hipEventCreate(&eb1));
@@ -536,8 +544,6 @@ int run_knnfit_overflow(int CS, const std::vector<FitFrame>& fr, const std::vect
     if (timing) {
         float bms = 0.0f;
         (void)hipEventElapsedTime(&bms, eb0, eb1);
-        (void)hipEventDestroy(eb0);
-        (void)hipEventDestroy(eb1);
         std::fprintf(stderr, "KNNFit overflow: %d trees (largest %d candidates), %zu queries, %.2f ms (tree builds %.2f ms)\n",
                      nt, max_n, jobs.size(), now_ms() - t_begin, double(bms));
     }
@@ -881,10 +887,6 @@ int Encoder::post_group(std::vector<FrameState>& frames, const std::vector<int>&
     for (int k = 0; k < g; ++k) {
         const size_t i = size_t(ids[k]);
         const FrameState& f = frames[i];
-        if (f.r > kMaxK) {
-            *err = "KNNFit: more than 4096 reduced chunks in a frame";
-            return -1;
-        }
         fit[size_t(k)] = FitFrame{c.coff[i], c.noff[i] * cs, c.noff[i], f.r, f.n, eps[size_t(k)], 0};
         pk[size_t(k)] = PackFrame{c.noff[i], c.roff[i], c.woff[i], f.n, f.r, 0, 0};
         maxN = std::max(maxN, f.n);
@@ -981,6 +983,17 @@ int Encoder::post_group(std::vector<FrameState>& frames, const std::vector<int>&
         const size_t i = size_t(ids[k]);
         frame_prune(frames[i], c.hCnt + c.roff[i], c.hRemap + c.roff[i]);
     });
+    // SaveStream's Assert(reducedChunks.Count <= CMaxChunksPerFrame) (encoder.lpr:986;
+    // built with assertions on): only a -pr0 passthrough frame (KNNFit over
+    // every chunk) can keep more than 4096 entries after pruning
+    for (int k = 0; k < g; ++k) {
+        const FrameState& f = frames[size_t(ids[k])];
+        if (f.r > kMaxK) {
+            *err = "SaveStream: Assert(reducedChunks.Count <= CMaxChunksPerFrame) failed: frame " +
+                   std::to_string(f.index) + " keeps " + std::to_string(f.r) + " reduced chunks";
+            return -1;
+        }
+    }
     ok = true;
     for (int k = 0; ok && k < g; ++k) {
         const size_t i = size_t(ids[k]);
@@ -1403,9 +1416,11 @@ int gsc_count_frames(const uint8_t* wav, size_t wav_len, const gsc_options* o, i
 }
 
 // encode frames [frame_begin, frame_end) of a prepared encoder into a
-// library-allocated buffer; timing lands in t_tim (host_prepare_ms excluded)
+// library-allocated buffer; timing lands in t_tim (host_prepare_ms excluded).
+// file_bytes: the range's bytes of every file of the batch; frame_bytes: each
+// frame's SaveStream bytes (frame_end - frame_begin entries)
 static int encode_prepared(Encoder& enc, int frame_begin, int frame_end, uint8_t** out, size_t* out_len,
-                           size_t* file_bytes = nullptr) {
+                           size_t* file_bytes = nullptr, size_t* frame_bytes = nullptr) {
     const double t0 = now_ms();
     const int fc = enc.frame_count();
     frame_begin = std::max(0, frame_begin);
@@ -1416,7 +1431,7 @@ static int encode_prepared(Encoder& enc, int frame_begin, int frame_end, uint8_t
     if (frame_end > frame_begin) {
         if (enc.encode_range(frame_begin, frame_end, &bytes, &err, &t_tim, nullptr, &fb) != 0) return fail(err);
     }
-    if (file_bytes) {  // the range's bytes of every file of the batch
+    if (file_bytes) {
         const std::vector<int>& ff = enc.file_first();
         for (size_t f = 0; f + 1 < ff.size(); ++f) {
             size_t n = 0;
@@ -1425,6 +1440,8 @@ static int encode_prepared(Encoder& enc, int frame_begin, int frame_end, uint8_t
             file_bytes[f] = n;
         }
     }
+    if (frame_bytes)
+        for (int i = frame_begin; i < frame_end; ++i) frame_bytes[i - frame_begin] = fb[size_t(i - frame_begin)];
     *out = static_cast<uint8_t*>(std::malloc(std::max<size_t>(bytes.size(), 1)));
     if (!*out) return fail("out of host memory");
     if (!bytes.empty()) std::memcpy(*out, bytes.data(), bytes.size());
@@ -1524,15 +1541,27 @@ gsc_prepared* gsc_prepare_frames(const uint8_t* wav, size_t wav_len, const gsc_o
     return p;
 }
 
+// every prepared entry point: a bounds-prepared encoder (gsc_prepare_frames)
+// holds only the samples of frames [loaded_begin, loaded_end)
+static int check_loaded(const gsc_prepared* p, int frame_begin, int frame_end, const char* who) {
+    if (p->loaded_end < 0) return 0;
+    const int fe = frame_end < 0 ? p->enc.frame_count() : std::min(frame_end, p->enc.frame_count());
+    const int fb = std::max(0, frame_begin);
+    if (fe > fb && (fb < p->loaded_begin || fe > p->loaded_end))
+        return fail(std::string(who) + ": frames outside the range gsc_prepare_frames loaded");
+    return 0;
+}
+
 int gsc_encode_prepared(gsc_prepared* p, int frame_begin, int frame_end, uint8_t** out, size_t* out_len) {
+    return gsc_encode_prepared_frames(p, frame_begin, frame_end, out, out_len, nullptr);
+}
+
+int gsc_encode_prepared_frames(gsc_prepared* p, int frame_begin, int frame_end, uint8_t** out, size_t* out_len,
+                               size_t* frame_bytes) {
     if (!p || !out || !out_len) return fail("gsc_encode_prepared: null argument");
-    if (p->loaded_end >= 0) {  // a bounds-prepared encoder holds only its own frames' samples
-        const int fe = frame_end < 0 ? p->enc.frame_count() : frame_end;
-        if (frame_begin < p->loaded_begin || fe > p->loaded_end)
-            return fail("gsc_encode_prepared: frames outside the range gsc_prepare_frames loaded");
-    }
+    if (check_loaded(p, frame_begin, frame_end, "gsc_encode_prepared") != 0) return -1;
     t_tim = gsc_timing{};
-    if (encode_prepared(p->enc, frame_begin, frame_end, out, out_len) != 0) return -1;
+    if (encode_prepared(p->enc, frame_begin, frame_end, out, out_len, nullptr, frame_bytes) != 0) return -1;
     t_tim.host_prepare_ms = 0;  // paid once, in gsc_prepare
     return 0;
 }
@@ -1572,6 +1601,7 @@ int gsc_prepared_file_frames(const gsc_prepared* p, int* first_frame) {
 int gsc_encode_prepared_files(gsc_prepared* p, int frame_begin, int frame_end, uint8_t** out, size_t* out_len,
                               size_t* file_bytes) {
     if (!p || !out || !out_len || !file_bytes) return fail("gsc_encode_prepared_files: null argument");
+    if (check_loaded(p, frame_begin, frame_end, "gsc_encode_prepared_files") != 0) return -1;
     t_tim = gsc_timing{};
     if (encode_prepared(p->enc, frame_begin, frame_end, out, out_len, file_bytes) != 0) return -1;
     return 0;

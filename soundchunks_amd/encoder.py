@@ -164,6 +164,21 @@ class Prepared:
         finally:
             lib.gsc_free(out)
 
+    def encode_frames(self, frame_begin: int = 0, frame_end: int = -1) -> tuple[bytes, list[int]]:
+        """Frames [frame_begin, frame_end): (bytes, each frame's byte count)."""
+        lib = _lib.load()
+        fe = self.frame_count if frame_end < 0 else min(frame_end, self.frame_count)
+        nb = max(0, fe - max(0, frame_begin))
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        ln = ctypes.c_size_t(0)
+        fb = (ctypes.c_size_t * max(1, nb))()
+        _lib.check(lib.gsc_encode_prepared_frames(self._h, frame_begin, frame_end, ctypes.byref(out),
+                                                  ctypes.byref(ln), fb))
+        try:
+            return ctypes.string_at(out, ln.value), [int(fb[i]) for i in range(nb)]
+        finally:
+            lib.gsc_free(out)
+
     def file_frames(self) -> np.ndarray:
         """First frame of every file of a batch, then the total frame count."""
         lib = _lib.load()

@@ -60,6 +60,19 @@ def _tone_lsb(seconds=4.5, rate=44100, seed=7):
     return wav_header(1, rate, n) + x.astype("<i2").tobytes()
 
 
+def _silence_burst(seconds=3.0, rate=44100):
+    """Mono digital silence with one 0.1-s tone burst: with -pr0 every chunk is
+    its own reduced chunk (passthrough, encoder.lpr:891-905), N ~ 16,500 > 4096,
+    but KNNFit maps the silent chunks onto one zero entry, so the pruned list
+    fits SaveStream's 4096 (encoder.lpr:986) and the reference encodes it."""
+    from soundchunks_amd.synth import wav_header
+
+    n = int(seconds * rate)
+    t = np.arange(n) / rate
+    x = np.where((t >= 1.0) & (t < 1.1), 0.25 * np.sin(2 * np.pi * 440 * t), 0.0)
+    return wav_header(1, rate, n) + np.round(x * 32767).astype("<i2").tobytes()
+
+
 def _tiny():
     """0.02 s: fewer chunks than ChunksPerFrame -> passthrough mode (encoder.lpr:891-912)."""
     return _synth(0.02)
@@ -88,6 +101,10 @@ CASES = {
     # cost loop (encoder.lpr:1337-1351) -- K = 485 and 1852 here, not powers of two
     "syn8s_br128_vfr05_cs8": (lambda: _synth(8.0), ["-br128", "-vfr0.5", "-cs8"]),
     "syn8s_br128_vfr05_cs16": (lambda: _synth(8.0), ["-br128", "-vfr0.5", "-cs16"]),
+    # -pr0 (Precision 0: passthrough, encoder.lpr:808) with more than 4096 chunks per frame:
+    # KNNFit over 4N candidates; quiet input keeps <= 4096 entries after pruning
+    "silence_burst_pr0_cs8": (lambda: _silence_burst(), ["-cs8", "-pr0"]),
+    "quiet_tone_pr0_cs4": (lambda: _quiet_tone(seconds=2.0, frac=0.97), ["-cs4", "-pr0"]),
     # a frame of more than 262,144 chunks (13-s frames at 48 kHz stereo -cs4: N ~ 312,000): yakmo's
     # chosen-point bitmap and prefix summaries live in HBM instead of LDS
     "syn13s_48k_cs4_cpf256_fl13000": (lambda: _synth(13.0, 48000), ["-cs4", "-cpf256", "-fl13000"]),

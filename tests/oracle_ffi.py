@@ -64,6 +64,11 @@ def load():
                                           ctypes.c_int, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t),
                                           ctypes.POINTER(ctypes.c_int)]
         lib.ora_encode_frames.restype = ctypes.c_int
+        lib.ora_encode_frame_list.argtypes = [u8p, ctypes.c_size_t, ctypes.POINTER(OraParams), ctypes.c_void_p,
+                                              ctypes.c_int, ctypes.c_int, ctypes.POINTER(u8p),
+                                              ctypes.POINTER(ctypes.c_size_t), ctypes.c_void_p,
+                                              ctypes.POINTER(ctypes.c_int)]
+        lib.ora_encode_frame_list.restype = ctypes.c_int
         lib.ora_encode_recon.argtypes = [u8p, ctypes.c_size_t, ctypes.POINTER(OraParams), ctypes.c_int,
                                          ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t),
                                          ctypes.POINTER(ctypes.POINTER(ctypes.c_int16)),
@@ -184,6 +189,31 @@ def encode_frames(wav: bytes, argv=(), frame_begin: int = 0, frame_end: int = -1
         return ctypes.string_at(out, n.value), fc.value
     finally:
         lib.ora_free(out)
+
+
+def encode_frame_list(wav: bytes, argv, frames, threads: int = 1):
+    """The listed frames of the whole-file encode: ([bytes of each frame], total frame count)."""
+    lib = load()
+    p = params(argv)
+    a, ptr = _u8(wav)
+    fl = np.ascontiguousarray(frames, dtype=np.int32)
+    fb = np.zeros(max(1, len(fl)), dtype=np.uint64)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t(0)
+    fc = ctypes.c_int(0)
+    rc = lib.ora_encode_frame_list(ptr, len(a), ctypes.byref(p), fl.ctypes.data, len(fl), threads, ctypes.byref(out),
+                                   ctypes.byref(n), fb.ctypes.data, ctypes.byref(fc))
+    if rc != 0:
+        raise RuntimeError(f"oracle encode failed: {rc}")
+    try:
+        blob = ctypes.string_at(out, n.value)
+    finally:
+        lib.ora_free(out)
+    parts, o = [], 0
+    for k in range(len(fl)):
+        parts.append(blob[o:o + int(fb[k])])
+        o += int(fb[k])
+    return parts, fc.value
 
 
 def scan_reduce(x, c0, precision=3, max_passes=100):

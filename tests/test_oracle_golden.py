@@ -19,13 +19,25 @@ import pytest
 import oracle_ffi
 from golden.cases import CASES, golden_path
 
-FAST = ["tiny_passthrough_cs8", "silence_tone_cs8_cpf256", "hihat_cs8_cpf256", "hihat_cs4_default"]
+FAST = ["tiny_passthrough_cs8", "silence_tone_cs8_cpf256", "hihat_cs8_cpf256", "hihat_cs4_default",
+        "silence_burst_pr0_cs8"]
 
 
 @pytest.mark.parametrize("name", FAST)
 def test_oracle_reproduces_golden(name):
     make, argv = CASES[name]
     assert oracle_ffi.encode(make(), argv, threads=4) == golden_path(name).read_bytes()
+
+
+def test_oracle_pr0_noise_fails_save_stream_assert():
+    """-pr0 on noise: every chunk is its own reduced chunk (passthrough,
+    encoder.lpr:891-905) and KNNFit keeps far more than 4096 of them, so
+    SaveStream's Assert(reducedChunks.Count <= CMaxChunksPerFrame)
+    (encoder.lpr:986, assertions on in encoder.lpi) stops the encode."""
+    from soundchunks_amd.synth import synth_wav
+
+    with pytest.raises(RuntimeError, match="-4"):
+        oracle_ffi.encode(synth_wav(1.0, 44100, 1), ["-cs8", "-pr0"], threads=2)
 
 
 def _frame_headers(gsc: bytes):

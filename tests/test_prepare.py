@@ -71,3 +71,56 @@ def test_prepare_frames_checks_bounds():
     bad[0] += 1  # not contiguous
     with pytest.raises(_lib.GscError):
         enc.prepare_frames(wav, st, bad, 0, 1)
+
+
+def test_every_prepared_entry_point_checks_the_loaded_range():
+    """A gsc_prepare_frames handle holds only its frames' samples: encoding
+    other frames through any entry point is an error, never an out-of-bounds
+    read (the check runs before any device work, so no GPU is needed)."""
+    import soundchunks_amd as sc
+    from soundchunks_amd import _lib
+
+    wav = synth_wav(20.0)
+    enc = sc.Encoder(["-cs8"])
+    st, en = enc.prepare(wav).frame_bounds()
+    q = enc.prepare_frames(wav, st, en, 1, 3)
+    for call in (lambda: q.encode(0, 2), lambda: q.encode(2, 4), lambda: q.encode(),
+                 lambda: q.encode_files(0, 1), lambda: q.encode_files(3, -1),
+                 lambda: q.encode_frames(0, 3)):
+        with pytest.raises(_lib.GscError, match="outside the range"):
+            call()
+
+
+def test_single_file_handles_are_one_file():
+    """gsc_prepare / gsc_prepare_frames handles report one file spanning every frame."""
+    import soundchunks_amd as sc
+
+    wav = synth_wav(20.0)
+    enc = sc.Encoder(["-cs8"])
+    p = enc.prepare(wav)
+    np.testing.assert_array_equal(p.file_frames(), [0, p.frame_count])
+    st, en = p.frame_bounds()
+    q = enc.prepare_frames(wav, st, en, 0, 2)
+    np.testing.assert_array_equal(q.file_frames(), [0, len(st)])
+
+
+def test_prepare_frames_accepts_an_empty_first_frame():
+    """The reference's cut can end frame 0 at i = 0 (encoder.lpr:1411-1417:
+    curPower >= perFramePower at the first block), leaving frame 0 = (0, -1);
+    broadcast bounds with that frame are valid."""
+    import soundchunks_amd as sc
+    from soundchunks_amd import _lib
+
+    wav = synth_wav(20.0)
+    enc = sc.Encoder(["-cs8"])
+    st, en = enc.prepare(wav).frame_bounds()
+    st2 = np.concatenate([[0], st]).astype(np.int32)
+    en2 = np.concatenate([[-1], en]).astype(np.int32)
+    q = enc.prepare_frames(wav, st2, en2, 1, 3)
+    assert q.frame_count == len(st) + 1
+    bad_s = np.concatenate([st[:1], [0], st[1:]]).astype(np.int32)  # an empty frame later on is still refused
+    bad_e = np.concatenate([en[:1], [en[0]], en[1:]]).astype(np.int32)
+    bad_e[1] = st[1] - 1
+    bad_s[1] = st[1]
+    with pytest.raises(_lib.GscError):
+        enc.prepare_frames(wav, bad_s, bad_e, 0, 1)
