@@ -13,6 +13,16 @@ constexpr int kMaxInternal = 4095; // internal kd nodes for K <= 4096 (heap inde
 constexpr int kScanThreads = 512;  // 8 waves, 2 per SIMD
 constexpr int kScanSlots = 8;      // kd leaves (centroids) per lane, 512*8 = 4096
 constexpr int kMaxScanIters = 100; // CMaxIterations (encoder.lpr:703)
+constexpr int kMaxChunkSize = 16;  // ChunkSize up to 16: 2*CS <= 32 features (-cs is unclamped, encoder.lpr:1992)
+
+// Row stride of the feature slab (Dataset, encoder.lpr:799-806) for a
+// ChunkSize: the 2*CS features padded with zeros to the next kernel width
+// 8 / 16 / 32.  Trailing zero features change no f32 distance, norm, mean or
+// move (x + 0*0 = x, (0 - 0)*rate + 0 = 0, exactly), ANN never splits on a
+// zero-spread dimension while a real one has spread (annMaxSpread keeps the
+// first maximum), and the residual divides by the real colCount (dcol), so
+// the padded search is the reference's search on the real features.
+__host__ __device__ constexpr int feature_stride(int cs) { return 2 * cs <= 8 ? 8 : (2 * cs <= 16 ? 16 : 32); }
 
 // One frame of TFrame.Reduce / KNNScanReduce work (encoder.lpr:785-913, 699-765).
 struct ReduceFrame {
@@ -32,6 +42,7 @@ struct ReduceFrame {
     int32_t loop_iters;   // out: batched-pipeline iterations (diagnostic); -1 = guard tripped
     int32_t tree_exact;   // out: passes whose kd-tree needed the sequential build (median ties)
     int32_t xseq;         // two-CU frames: tag of the last hand-off between the two CUs
+    int32_t dcol;         // colCount = 2*ChunkSize (the residual's divisor, encoder.lpr:743); 0 = the slab width
     uint64_t t_done;      // out: s_memrealtime (100 MHz) when the batched kernel finished the frame
     // optional (batched kernel): when the frame is done, its final clusters are
     // copied to cl_host (host-mapped, N ints) and then *notify is set (system
@@ -47,7 +58,7 @@ struct ReduceFrame {
 // (encoder.lpr:566-605) and the MakeChunks features (encoder.lpr:467-485).
 struct DspFrame {
     int64_t s_off;        // first sample of the frame in each channel row of the sample slab
-    int64_t x_off;        // features out: n*2CS floats at X + x_off (chunk-major, channel-minor)
+    int64_t x_off;        // features out: n*feature_stride(CS) floats at X + x_off (chunk-major, channel-minor)
     int64_t c_off;        // per-chunk bytes out (neg | rev << 1) at +c_off
     int32_t sc;           // frame sample count
     int32_t n;            // chunks (chunk_count * channels)

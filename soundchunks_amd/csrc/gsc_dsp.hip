@@ -46,14 +46,17 @@ __device__ __forceinline__ int ceil_pos_i32(double x) {
 // the same sequential chain, so the result is unchanged; the f64 latency
 // chains now run on all four SIMDs instead of one.
 constexpr int kAttProd = 7;                  // producer waves
-constexpr int kAttBatch = kAttProd * 16;     // samples per batch: whole chunks for CS = 4, 8, 16
+constexpr int kAttBatchMax = kAttProd * 16;  // samples per batch (LDS: two buffers of 64 lanes x f64)
 constexpr int kAttThreads = 64 * (kAttProd + 1);
+// samples per batch for a ChunkSize: whole chunks, the same number per producer
+__host__ __device__ constexpr int att_batch(int cs) { return kAttProd * cs * (cs >= 16 ? 1 : 16 / cs); }
 
 template <int CS>
 __global__ __launch_bounds__(kAttThreads) void atten_kernel(DspFrame* __restrict__ frames, int nframes,
                                                             const double* __restrict__ samp, int64_t span, int ch,
                                                             int obd) {
-    static_assert(kAttBatch % (CS * kAttProd) == 0, "whole chunks per producer");
+    constexpr int kAttBatch = att_batch(CS);
+    static_assert(kAttBatch % (CS * kAttProd) == 0 && kAttBatch <= kAttBatchMax, "whole chunks per producer");
     extern __shared__ __attribute__((aligned(16))) double aterm[];  // [2][kAttBatch][64]
     const int fi = blockIdx.x;
     if (fi >= nframes) return;
@@ -171,6 +174,7 @@ __global__ __launch_bounds__(256) void features_kernel(const DspFrame* __restric
     const DspFrame fr = frames[fi];
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= fr.n) return;
+    constexpr int DP = feature_stride(CS);  // slab row: 2*CS features, then zeros
     const int i = c / ch, j = c - i * ch;
     // chunk samples, zero past the frame end (encoder.lpr:467-485: 0 + sample)
     double s[CS];
@@ -205,7 +209,9 @@ __global__ __launch_bounds__(256) void features_kernel(const DspFrame* __restric
     double data[CS], temp[CS];
 #pragma unroll
     for (int k = 0; k < CS; ++k) data[k] = s[rev ? CS - 1 - k : k] * (neg ? -1.0 : 1.0);
-    float* out = X + fr.x_off + int64_t(c) * 2 * CS;
+    float* out = X + fr.x_off + int64_t(c) * DP;
+#pragma unroll
+    for (int k = 2 * CS; k < DP; ++k) out[k] = 0.0f;
     // DCT-II (encoder.lpr:258-276)
 #pragma unroll
     for (int k = 0; k < CS; ++k) {
@@ -271,7 +277,7 @@ extern "C" hipError_t gsc_launch_pcm(const int16_t* pcm, int64_t span, int ch, d
 // FindAttenuationDivider for every frame (one 8-wave workgroup per frame)
 extern "C" hipError_t gsc_launch_atten(int cs, DspFrame* frames, int nframes, const double* samp, int64_t span, int ch,
                                        int obd, hipStream_t st) {
-    const size_t shm = size_t(2) * kAttBatch * 64 * sizeof(double);
+    const size_t shm = size_t(2) * att_batch(cs) * 64 * sizeof(double);
     switch (cs) {
 #define AK(CSV)                                                                                                  \
     case CSV:                                                                                                    \
@@ -281,24 +287,27 @@ extern "C" hipError_t gsc_launch_atten(int cs, DspFrame* frames, int nframes, co
         hipLaunchKernelGGL(atten_kernel<CSV>, dim3(nframes), dim3(kAttThreads), shm, st, frames, nframes, samp,  \
                            span, ch, obd);                                                                       \
         break;
-        AK(4)
-        AK(8)
-        AK(16)
+        AK(1) AK(2) AK(3) AK(4) AK(5) AK(6) AK(7) AK(8) AK(9) AK(10) AK(11) AK(12) AK(13) AK(14) AK(15) AK(16)
 #undef AK
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
 
-// chunk features for every frame; trig = 5 CS x CS f64 tables (dct, dft cos/sin, idft cos/sin)
+// chunk features for every frame (slab rows of feature_stride(CS) floats); trig = 5 CS x CS f64 tables
+// (dct, dft cos/sin, idft cos/sin)
 extern "C" hipError_t gsc_launch_features(int cs, const DspFrame* frames, int nframes, int max_n, const double* samp,
                                           int64_t span, int ch, const double* trig, double s0, double scale, float* X,
                                           uint8_t* nr, float* Q, hipStream_t st) {
     const dim3 grid((max_n + 255) / 256, nframes), block(256);
     switch (cs) {
-    case 4: hipLaunchKernelGGL(features_kernel<4>, grid, block, 0, st, frames, nframes, samp, span, ch, trig, s0, scale, X, nr, Q); break;
-    case 8: hipLaunchKernelGGL(features_kernel<8>, grid, block, 0, st, frames, nframes, samp, span, ch, trig, s0, scale, X, nr, Q); break;
-    case 16: hipLaunchKernelGGL(features_kernel<16>, grid, block, 0, st, frames, nframes, samp, span, ch, trig, s0, scale, X, nr, Q); break;
+#define FK(CSV)                                                                                                  \
+    case CSV:                                                                                                    \
+        hipLaunchKernelGGL(features_kernel<CSV>, grid, block, 0, st, frames, nframes, samp, span, ch, trig, s0,   \
+                           scale, X, nr, Q);                                                                     \
+        break;
+        FK(1) FK(2) FK(3) FK(4) FK(5) FK(6) FK(7) FK(8) FK(9) FK(10) FK(11) FK(12) FK(13) FK(14) FK(15) FK(16)
+#undef FK
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -10,6 +10,7 @@
 #include <cstring>
 
 #include "fpc_math.h"
+#include "gsc_device.h"
 #include "gsc_seqsum.h"
 
 namespace gsc {
@@ -171,8 +172,10 @@ int Encoder::load(const uint8_t* wav, size_t len, int64_t s0, int64_t s1, std::s
         *err = "ChunkBitDepth must be 8 or 12 (TFrame.SaveStream)";
         return -2;
     }
-    if (!(o.chunk_size == 4 || o.chunk_size == 8 || o.chunk_size == 16)) {
-        *err = "ChunkSize must be 4, 8 or 16";
+    // -cs is unclamped in the reference (encoder.lpr:1992); the kernels take
+    // 2*ChunkSize <= 32 features (padded to 8 / 16 / 32, gsc_device.h feature_stride)
+    if (o.chunk_size < 1 || o.chunk_size > kMaxChunkSize) {
+        *err = "ChunkSize must be 1..16 (2*ChunkSize <= 32 features)";
         return -2;
     }
     const int cs = o.chunk_size, ch = channels_;

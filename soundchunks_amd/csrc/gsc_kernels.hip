@@ -109,11 +109,14 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
     const int pass = uniform_int(frp->iters);  // frames advance on their own pass counts
     if (pass >= max_passes) return;
     const int N = uniform_int(frp->N), K = uniform_int(frp->K);
-    const float* __restrict__ X = uniform_ptr(Xall + frp->x_off);
-    float* C = uniform_ptr(Call + frp->c_off);
-    int* clusters = uniform_ptr(i_scratch + frp->n_off);
-    int* prev_cnt = uniform_ptr(i_scratch + frp->k_off);  // cnts[not Odd(iter)] by centroid id
-    float* box0 = uniform_ptr(f_scratch + frp->n_off * 3);  // root box per query (yakmo scratch reused)
+    const int dcol_i = uniform_int(frp->dcol) > 0 ? uniform_int(frp->dcol) : D;
+    // best / colCount: a constant power-of-two divisor (an exact multiply) unless the slab is padded
+    auto per_col = [dcol_i](float v) { return dcol_i == D ? v / (float)D : v / (float)dcol_i; };
+    const float* __restrict__ X = Xall + uniform_i64(frp->x_off);
+    float* C = Call + uniform_i64(frp->c_off);
+    int* clusters = i_scratch + uniform_i64(frp->n_off);
+    int* prev_cnt = i_scratch + uniform_i64(frp->k_off);  // cnts[not Odd(iter)] by centroid id
+    float* box0 = f_scratch + uniform_i64(frp->n_off * 3);  // root box per query (yakmo scratch reused)
     int* first = reinterpret_cast<int*>(box0 + N);            // first leaf of ANN's descent per query
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nthreads = blockDim.x, nwaves = nthreads >> 6;
@@ -402,7 +405,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
             if (me) sh.cnta[bpos] += 1;
             if (tid == 0) {
                 clusters[i] = id;
-                err += (double)__fsqrt_rn(bkey / (float)D);
+                err += (double)__fsqrt_rn(per_col(bkey));
             }
         }
     }
@@ -612,9 +615,7 @@ extern "C" hipError_t gsc_launch_knnfit(int CS, FitFrame* frames, int nframes, i
             return e;                                                                                             \
         hipLaunchKernelGGL(knnfit_kernel<CSV>, grid, block, shm, st, frames, nframes, cand, q, out, tiles, tile_r);          \
         break;
-        KF(4)
-        KF(8)
-        KF(16)
+        KF(1) KF(2) KF(3) KF(4) KF(5) KF(6) KF(7) KF(8) KF(9) KF(10) KF(11) KF(12) KF(13) KF(14) KF(15) KF(16)
 #undef KF
     default: return hipErrorInvalidValue;
     }

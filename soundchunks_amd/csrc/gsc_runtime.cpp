@@ -293,10 +293,12 @@ std::vector<float> rate_table(int n) {
 // cl_host / notify (optional, device pointers of host-mapped memory): the
 // batched kernel copies a frame's final clusters to cl_host + its n_off and
 // then sets notify[i], so the host can post-process it during the scan tail
+// D: the slab's row width (8, 16 or 32); dcol: the real colCount 2*ChunkSize
+// (<= D, trailing features zero; 0 = D)
 int run_reduce_batch_dev(int D, int K, int precision, const std::vector<int>& Ns, const std::vector<int64_t>& xoff,
                          const float* dX, std::vector<float>* C, std::vector<int>* clusters, std::vector<int>* iters,
                          std::vector<int>* slow, long long* restarts, double* yakmo_ms, double* scan_ms,
-                         int* cl_host = nullptr, int* notify = nullptr) {
+                         int* cl_host = nullptr, int* notify = nullptr, int dcol = 0) {
     // launches: one yakmo launch + kMaxScanIters scan launches per batch
     const int nf = int(Ns.size());
     if (nf == 0) return 0;
@@ -311,6 +313,7 @@ int run_reduce_batch_dev(int D, int K, int precision, const std::vector<int>& Ns
         fr[i].k_off = 0;  // filled below
         fr[i].N = Ns[i];
         fr[i].K = K;
+        fr[i].dcol = dcol;
         no += Ns[i];
         maxN = std::max<int64_t>(maxN, Ns[i]);
     }
@@ -684,6 +687,14 @@ struct PostCtx {
     }
 };
 
+// rows of `dp` floats (the device slab) -> rows of the first `d` of them
+static void compact_rows(std::vector<float>* v, int n, int dp, int d) {
+    if (dp == d) return;
+    for (int i = 0; i < n; ++i)
+        for (int k = 0; k < d; ++k) (*v)[size_t(i) * d + k] = (*v)[size_t(i) * dp + k];
+    v->resize(size_t(n) * d);
+}
+
 // ---- Encoder::device_dsp: FindAttenuationDivider + features on the device --
 // dXv: DevBuf<float>* that receives the feature slab (kept for the Reduce).
 int Encoder::device_dsp(int b, std::vector<FrameState>& frames, void* dXv, std::vector<int64_t>* xoff, double* ms,
@@ -706,7 +717,7 @@ int Encoder::device_dsp(int b, std::vector<FrameState>& frames, void* dXv, std::
         df[i].sc = f.sample_count;
         df[i].n = f.n;
         (*xoff)[i] = xo;
-        xo += int64_t(f.n) * 2 * cs;
+        xo += int64_t(f.n) * feature_stride(cs);
         co += f.n;
         max_n = std::max(max_n, f.n);
     }
@@ -1065,11 +1076,13 @@ int Encoder::dsp_frame(int fi, int* atten_div, std::vector<float>* feat, std::st
     std::vector<int64_t> xoff;
     if (device_dsp(fi, frames, &dX, &xoff, nullptr, err) != 0) return -1;
     *atten_div = frames[0].atten_div;
-    feat->resize(size_t(frames[0].n) * 2 * opt_.chunk_size);
+    const int dp = feature_stride(opt_.chunk_size);
+    feat->resize(size_t(frames[0].n) * dp);
     if (hipMemcpy(feat->data(), dX.p, sizeof(float) * feat->size(), hipMemcpyDeviceToHost) != hipSuccess) {
         *err = "feature download failed";
         return -1;
     }
+    compact_rows(feat, frames[0].n, dp, 2 * opt_.chunk_size);
     return 0;
 }
 
@@ -1081,6 +1094,7 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
         return -1;
     }
     const int cs = opt_.chunk_size, D = 2 * cs, K = opt_.chunks_per_frame;
+    const int DP = feature_stride(cs);  // the feature slab's row width (D features, then zeros)
     const int nfr = e - b;
     std::vector<FrameState> frames(static_cast<size_t>(std::max(nfr, 0)));
     double t0 = now_ms();
@@ -1227,12 +1241,13 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
         const double tb = now_ms();
         for (size_t j = 0; j < red_idx.size(); ++j) {
             FrameState& f = frames[red_idx[j]];
-            std::vector<float> x(size_t(f.n) * D);
+            std::vector<float> x(size_t(f.n) * DP);
             if (hipMemcpy(x.data(), dFeat.p + red_xoff[j], sizeof(float) * x.size(), hipMemcpyDeviceToHost) !=
                 hipSuccess) {
                 *err = "-py: feature download failed";
                 return -1;
             }
+            compact_rows(&x, f.n, DP, D);  // cluster.py reads the real features (extern.pas:363-369)
             f.clusters.resize(size_t(f.n));
             if (birch_reduce_labels(f.n, D, x.data(), K, f.clusters.data(), err) != 0) return -1;
             f.scan_iters = 0;
@@ -1262,8 +1277,8 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
             hipHostGetDevicePointer(reinterpret_cast<void**>(&nt_dev), notify, 0) != hipSuccess) {
             rr = fail("KNNScanReduce: no device address for the host-mapped cluster buffers");
         } else {
-            rr = run_reduce_batch_dev(D, K, opt_.precision, Ns, red_xoff, dFeat.p, &C, &cl_final, &it, &sl, &restarts,
-                                      &yak_ms, &scan_ms, cl_dev, nt_dev);
+            rr = run_reduce_batch_dev(DP, K, opt_.precision, Ns, red_xoff, dFeat.p, &C, &cl_final, &it, &sl, &restarts,
+                                      &yak_ms, &scan_ms, cl_dev, nt_dev, D);
         }
         t_scan_end = now_ms();
         if (rr != 0) *err = t_err;
@@ -1680,10 +1695,19 @@ int gsc_encode_wav_recon(const uint8_t* wav, size_t wav_len, const gsc_options* 
     return 0;
 }
 
-int gsc_yakmo_seed_means(int n, int d, const float* x, int k, float* centroids) {
+// rows of d floats -> rows of dp (trailing zeros)
+static std::vector<float> pad_rows(const float* x, int n, int d, int dp) {
+    std::vector<float> v(size_t(n) * dp, 0.0f);
+    for (int i = 0; i < n; ++i) std::memcpy(&v[size_t(i) * dp], x + size_t(i) * d, sizeof(float) * size_t(d));
+    return v;
+}
+
+int gsc_yakmo_seed_means(int n, int d0, const float* x, int k, float* centroids) {
     if (ensure_device() != 0) return -1;
     if (k >= n || k <= 0 || k > kMaxK) return fail("yakmo needs 0 < k < n, k <= 4096");
-    std::vector<float> X(x, x + size_t(n) * d), C;
+    if (d0 <= 0 || d0 > 32) return fail("yakmo: 1 <= d <= 32 features");
+    const int d = feature_stride((d0 + 1) / 2);  // the kernel width; trailing zero features change nothing
+    std::vector<float> X = pad_rows(x, n, d0, d), C;
     std::vector<int> cl, it, sl;
     // run only the seeding part: precision 0 => scan loop still runs once; use a
     // dedicated path instead
@@ -1708,23 +1732,30 @@ int gsc_yakmo_seed_means(int n, int d, const float* x, int k, float* centroids) 
     HIP_TRY(hipMemcpy(dFr.p, fr.data(), sizeof(ReduceFrame), hipMemcpyHostToDevice));
     HIP_TRY(gsc_launch_yakmo(d, dFr.p, nf, dX.p, dC.p, dF.p, dI.p, dYSum.p, dBits.p, n, nullptr));
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(centroids, dC.p, sizeof(float) * size_t(k) * d, hipMemcpyDeviceToHost));
-    (void)C;
+    C.resize(size_t(k) * d);
+    HIP_TRY(hipMemcpy(C.data(), dC.p, sizeof(float) * size_t(k) * d, hipMemcpyDeviceToHost));
+    compact_rows(&C, k, d, d0);
+    std::memcpy(centroids, C.data(), sizeof(float) * size_t(k) * d0);
     (void)cl;
     (void)it;
     (void)sl;
     return 0;
 }
 
-int gsc_scan_reduce(int n, int d, const float* x, int k, float* centroids, int* clusters, int precision, int* iters) {
+int gsc_scan_reduce(int n, int d0, const float* x, int k, float* centroids, int* clusters, int precision, int* iters) {
     if (ensure_device() != 0) return -1;
     // same kernels as the encoder, but starting from caller-provided centroids:
     // seed via yakmo is skipped by uploading the centroids after the yakmo launch
-    if (d != 8 && d != 16 && d != 32) return fail("KNNScanReduce kernels support D = 8, 16 or 32");
+    if (d0 <= 0 || d0 > 32) return fail("KNNScanReduce kernels support 1 <= d <= 32 features");
+    const int d = feature_stride((d0 + 1) / 2);  // padded with zero features (residual divides by d0)
+    const std::vector<float> xp = pad_rows(x, n, d0, d);
+    std::vector<float> cp = pad_rows(centroids, k, d0, d);
+    x = xp.data();
     std::vector<ReduceFrame> fr(1);
     fr[0] = ReduceFrame{};
     fr[0].N = n;
     fr[0].K = k;
+    fr[0].dcol = d0;
     fr[0].k_off = n;
     fr[0].ka_off = n + k;
     DevBuf<float> dX, dC, dRate, dF;
@@ -1738,12 +1769,14 @@ int gsc_scan_reduce(int n, int d, const float* x, int k, float* centroids, int* 
     const std::vector<float> rt = rate_table(n);
     HIP_TRY(dRate.alloc(rt.size()));
     HIP_TRY(hipMemcpy(dX.p, x, sizeof(float) * size_t(n) * d, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(dC.p, centroids, sizeof(float) * size_t(k) * d, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dC.p, cp.data(), sizeof(float) * size_t(k) * d, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(dRate.p, rt.data(), sizeof(float) * rt.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(dFr.p, fr.data(), sizeof(ReduceFrame), hipMemcpyHostToDevice));
     HIP_TRY(launch_scan_passes(d, dFr.p, 1, k, dX.p, dC.p, dI.p, dF.p, dRate.p, precision));
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(centroids, dC.p, sizeof(float) * size_t(k) * d, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(cp.data(), dC.p, sizeof(float) * size_t(k) * d, hipMemcpyDeviceToHost));
+    compact_rows(&cp, k, d, d0);
+    std::memcpy(centroids, cp.data(), sizeof(float) * size_t(k) * d0);
     HIP_TRY(hipMemcpy(clusters, dI.p, sizeof(int) * size_t(n), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(fr.data(), dFr.p, sizeof(ReduceFrame), hipMemcpyDeviceToHost));
     if (iters) *iters = fr[0].iters;

@@ -273,6 +273,17 @@ __device__ __forceinline__ uint32_t sum16(uint32_t v) {
 
 __device__ __forceinline__ int wave_of_lane() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
+// the lane index as a value the compiler cannot see through: refreshed at the
+// phase boundaries of the scan loop, so every per-lane LDS address is computed
+// where it is used (one VALU op) instead of being hoisted out of the loop,
+// kept live through A1 and spilled to scratch (a scratch reload is a
+// vector-memory round trip, and its vmcnt wait also waits for the query
+// prefetch from HBM)
+__device__ __forceinline__ int opaque_v(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
 // orders this wave's LDS accesses across lanes (lane-to-lane hand-off
 // through LDS inside one wave: without it the compiler may reorder them)
 __device__ __forceinline__ void wave_lds_sync() {
@@ -423,8 +434,11 @@ __device__ __forceinline__ float wave_box_lb(const Scan2Shared<C>& sh, const flo
     float lb = 0.0f;
 #pragma unroll
     for (int d = 0; d < C::D; ++d) {
+        // branch-free: lo - qd > 0 below the box, qd - hi > 0 above it, else 0
+        // (an empty box, lo = +inf > hi = -inf, gives +inf either way); the
+        // selected difference is the same f32 value as a branchy select
         const float qd = q[d], lo = sh.wlo[w][d], hi = sh.whi[w][d];
-        const float t = lo > qd ? fsub(lo, qd) : (qd > hi ? fsub(qd, hi) : 0.0f);
+        const float t = fmaxf(fmaxf(fsub(lo, qd), fsub(qd, hi)), 0.0f);
         lb = fadd(lb, fmul(t, t));
     }
     return fmul(lb, 1.0f - 0x1p-17f);
@@ -1418,18 +1432,22 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     ReduceFrame* frp = frames + fi;
     if (uniform_int(frp->done) || uniform_int(frp->generic)) continue;
     const int N = uniform_int(frp->N);
+    // colCount of the residual (encoder.lpr:743): 2*ChunkSize, below D when the slab pads the features
+    const int dcol_i = uniform_int(frp->dcol) > 0 ? uniform_int(frp->dcol) : D;
+    // best / colCount: a constant power-of-two divisor (an exact multiply) unless the slab is padded
+    auto per_col = [dcol_i](float v) { return dcol_i == D ? v / (float)D : v / (float)dcol_i; };
     // ChunksPerFrame that is not a power of two (the -br cost loop,
     // encoder.lpr:1337-1351): ANN's tree over the Kr centroids, embedded in the
     // K = 2^LOGK leaf layout with padding leaves that are never visited (pad_tree)
     const int Kr = NWG == 1 ? uniform_int(frp->K) : K;
     const bool padded = Kr != K;
-    const float* __restrict__ X = uniform_ptr(Xall + frp->x_off);
-    float* C_ = uniform_ptr(Call + frp->c_off);
-    int* clusters = uniform_ptr(i_scratch + frp->n_off);
-    int* prev_cnt = uniform_ptr(i_scratch + frp->k_off);  // cnts[not Odd(iter)] by centroid id
-    int* cnta = uniform_ptr(i_scratch + frp->ka_off);     // cnts[Odd(iter)] by kd-leaf position
+    const float* __restrict__ X = Xall + uniform_i64(frp->x_off);
+    float* C_ = Call + uniform_i64(frp->c_off);
+    int* clusters = i_scratch + uniform_i64(frp->n_off);
+    int* prev_cnt = i_scratch + uniform_i64(frp->k_off);  // cnts[not Odd(iter)] by centroid id
+    int* cnta = i_scratch + uniform_i64(frp->ka_off);     // cnts[Odd(iter)] by kd-leaf position
     // split layout: the tail features of kd-leaf position p at trow + p * TL
-    float* trow = C::SPLIT ? uniform_ptr(Tall + frp->t_off) : nullptr;
+    float* trow = C::SPLIT ? Tall + uniform_i64(frp->t_off) : nullptr;
     XPort xp{nullptr, nullptr, 0};
     if constexpr (NWG == 2) {
         xp.mine = xbuf + ((size_t)fi * 2 + wg) * 2 * kXCap;
@@ -1691,9 +1709,18 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     int cur_buf = 0, cur_s = 0, cur_n = n0;  // batch whose distances are computed this iteration
     int next_load = n0;
     for (int it = 0;; ++it) {
+        int ln = opaque_v(lane);  // see opaque_v: refreshed per phase below
         const bool has_p = nvq > 0;
         const int P_buf = vq_buf0, P_s = vq_s0, P_off = vq_off0, P_n = has_p ? vq_n0 : 0;
-        // prefetch the next batch's queries (they land in LDS in part 3)
+        // ---- part 1: chain the pending batch's updates (wave 0); A1(current)
+        VPState vst;
+#ifdef GSC_STAMPS_PREP
+        STAMP(14)  // diagnostic split of "prep": loop top (into a2box's slot) vs the update chain
+#endif
+        if (wave == 0 && has_p) vp_begin<C>(sh, P_buf, P_off, P_n, vq_a10, ln, lg_pos, lg_tag, vst);
+        // prefetch the next batch's queries (they land in LDS in part 3).  Issued
+        // after vp_begin: a wait for any later vector-memory op (a scratch reload)
+        // waits for this HBM load too, and A1 below issues none
         constexpr int PE = (KB * D + nthreads - 1) / nthreads;
         float pre[PE];
 #pragma unroll
@@ -1701,12 +1728,6 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             const int k = tid + e * nthreads;
             pre[e] = (k < KB * D && next_load + k / D < N) ? X[(int64_t)next_load * D + k] : 0.0f;
         }
-        // ---- part 1: chain the pending batch's updates (wave 0); A1(current)
-        VPState vst;
-#ifdef GSC_STAMPS_PREP
-        STAMP(14)  // diagnostic split of "prep": loop top (into a2box's slot) vs the update chain
-#endif
-        if (wave == 0 && has_p) vp_begin<C>(sh, P_buf, P_off, P_n, vq_a10, lane, lg_pos, lg_tag, vst);
         STAMP(0)
         // A1 of the queries in mask m, two per trip: one query's min-tree (a
         // dependent DPP chain) overlaps the other's distance FMAs
@@ -1722,17 +1743,17 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                     a1_dist_x2<C::H, C::DR, SL>(creg, cn, sh.qm[cur_buf][j0], sh.qm[cur_buf][j1], dv0, dv1);
                 else if constexpr (!C::SPLIT)
                     a1_dist_x2<D, D, SL>(creg, cn, sh.qm[cur_buf][j0], sh.qm[cur_buf][j1], dv0, dv1);
-                a1_reduce2<C>(dv0, dv1, sh.wrec[vwave][j0], sh.wrec[vwave][j1], vwave, lane);
+                a1_reduce2<C>(dv0, dv1, sh.wrec[vwave][j0], sh.wrec[vwave][j1], vwave, ln);
             }
         };
         const uint64_t curm = cur_n > 0 ? (cur_n >= 64 ? ~0ull : (1ull << cur_n) - 1ull) : 0ull;
         uint64_t prunedm = 0;  // queries this wave skipped (wave-uniform)
-        float lbp = 0.0f, qn_j = 0.0f, eps_j = 0.0f;  // lane j: query j's box bound, |q|^2, eps
+        float lbp = 0.0f, qn_j = 0.0f, eps_j = 0.0f;  // ln j: query j's box bound, |q|^2, eps
         if constexpr (PRUNE) {
             if (no_prune) {
                 a1_mask(curm);
             } else if (cur_n > 0) {
-                const int jr = lane < cur_n ? lane : 0;
+                const int jr = ln < cur_n ? ln : 0;
                 const float* qv = sh.q[cur_buf][jr];
                 lbp = wave_box_lb<C>(sh, qv, vwave);
                 qn_j = half ? norm2_x<C::H>(qv) : norm2_x<D>(qv);
@@ -1746,10 +1767,10 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 const uint64_t home = __ballot(lbp == 0.0f) & curm;
                 a1_mask(home);
                 wave_lds_sync();
-                if ((home >> lane) & 1ull) {
-                    const float m = __uint_as_float(sh.wrec[vwave][lane].minbits);
+                if ((home >> ln) & 1ull) {
+                    const float m = __uint_as_float(sh.wrec[vwave][ln].minbits);
                     const float ubd = fmul(fadd(fadd(qn_j, m), eps_j), 1.0f + 0x1p-20f);
-                    atomicMin(&sh.ub[lane], __float_as_uint(fmaxf(ubd, 0.0f)));
+                    atomicMin(&sh.ub[ln], __float_as_uint(fmaxf(ubd, 0.0f)));
                 }
                 lds_barrier();
                 const float ubj = __uint_as_float(sh.ub[jr]);
@@ -1760,14 +1781,14 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 acn[1] += __popcll(prunedm);
                 acn[2] += __popcll(curm & ~home & ~prunedm);
 #endif
-                if ((prunedm >> lane) & 1ull)  // a lower bound of this wave's A1 values (see above)
-                    sh.wrec[vwave][lane].minbits = __float_as_uint(fsub(fsub(lbp, fmul(3.0f, eps_j)), qn_j));
+                if ((prunedm >> ln) & 1ull)  // a lower bound of this wave's A1 values (see above)
+                    sh.wrec[vwave][ln].minbits = __float_as_uint(fsub(fsub(lbp, fmul(3.0f, eps_j)), qn_j));
                 a1_mask(curm & ~home & ~prunedm);
             }
         } else {
             a1_mask(curm);
         }
-        if (wave == 0 && has_p) vp_end<C>(sh, P_buf, P_off, P_n, lane, lg_pos, vst);
+        if (wave == 0 && has_p) vp_end<C>(sh, P_buf, P_off, P_n, ln, lg_pos, vst);
 #ifdef GSC_STAMPS
         acn[3] += 1;
         acn[5] += P_n;
@@ -1777,7 +1798,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         STAMP(6)
         if constexpr (NWG == 2) {
             if (cur_n > 0) {
-                write_cstar<C>(sh, creg, sh.qrec[cur_buf], (1ull << cur_n) - 1ull, 0, wave, lane, wg);
+                write_cstar<C>(sh, creg, sh.qrec[cur_buf], (1ull << cur_n) - 1ull, 0, wave, ln, wg);
                 lds_barrier();
                 xchg_records<C>(sh, xp, cur_n, nullptr, 0, sh.qrec[cur_buf], tid, wg);
                 lds_barrier();
@@ -1785,16 +1806,17 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             }
         }
         // ---- part 2: check the pending batch; certificates of the current batch
-        if (has_p) v_check_q<C>(sh, P_buf, P_off, P_n, wave, lane);
+        ln = opaque_v(ln);
+        if (has_p) v_check_q<C>(sh, P_buf, P_off, P_n, wave, ln);
         STAMP(7)
         if (cur_n > 0) {
             // c*'s snapshot coordinates (and exact distance), written by the wave that owns c*
             if constexpr (NWG == 1)
-                write_cstar<C>(sh, creg, sh.qrec[cur_buf], (1ull << cur_n) - 1ull, 0, wave, lane, 0, trow);
+                write_cstar<C>(sh, creg, sh.qrec[cur_buf], (1ull << cur_n) - 1ull, 0, wave, ln, 0, trow);
             STAMP(8)
 #pragma unroll 1
             for (int j0 = wave * 4; j0 < cur_n; j0 += 4 * NWL)
-                a2_group<C, true>(sh, j0, cur_n, sh.q[cur_buf], sh.qrec[cur_buf], 0, nullptr, lane, half, twh, te,
+                a2_group<C, true>(sh, j0, cur_n, sh.q[cur_buf], sh.qrec[cur_buf], 0, nullptr, ln, half, twh, te,
                                   nan_rows != 0
 #ifdef GSC_STAMPS
                                   , acc, &tlast
@@ -1806,59 +1828,60 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         if (cur_n > 0) {
             // queries the approximate certificate could not decide: exact A1 + A2
             // on the same snapshot (the registers change only in part 4)
-            const uint64_t fx = __ballot(lane < cur_n && sh.qrec[cur_buf][lane].valid == 0);
+            const uint64_t fx = __ballot(ln < cur_n && sh.qrec[cur_buf][ln].valid == 0);
             if (fx) {
                 const int nfx = __popcll(fx);
 #ifdef GSC_STAMPS
                 acn[4] += nfx;
 #endif
-                if (wave == 0 && ((fx >> lane) & 1ull)) sh.fxl[__popcll(fx & ((1ull << lane) - 1ull))] = lane;
+                if (wave == 0 && ((fx >> ln) & 1ull)) sh.fxl[__popcll(fx & ((1ull << ln) - 1ull))] = ln;
                 uint64_t m = fx;
                 while (m) {
                     const int jj = __ffsll((long long)m) - 1;
                     m &= m - 1;
                     if ((prunedm >> jj) & 1ull) {  // still provably far: the exact record's lower bound
                         const float lb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbp), jj));
-                        if (lane == 0) sh.wrec[vwave][jj].minbits = __float_as_uint(lb);
+                        if (ln == 0) sh.wrec[vwave][jj].minbits = __float_as_uint(lb);
                     } else {
-                        a1_query<C>(creg, sh.q[cur_buf][jj], sh.wrec[vwave][jj], vwave, lane, dmask, trow, p0, tw_pass);
+                        a1_query<C>(creg, sh.q[cur_buf][jj], sh.wrec[vwave][jj], vwave, ln, dmask, trow, p0, tw_pass);
                     }
                 }
                 lds_barrier();
                 if constexpr (NWG == 2) {
-                    write_cstar<C>(sh, creg, sh.qrec[cur_buf], fx, 0, wave, lane, wg);
+                    write_cstar<C>(sh, creg, sh.qrec[cur_buf], fx, 0, wave, ln, wg);
                     lds_barrier();
                     xchg_records<C>(sh, xp, nfx, sh.fxl, 0, sh.qrec[cur_buf], tid, wg);
                     lds_barrier();
                     fill_winner_coords<C>(sh, sh.qrec[cur_buf], nfx, sh.fxl, 0, tid, wg);
                 } else {
-                    write_cstar<C>(sh, creg, sh.qrec[cur_buf], fx, 0, wave, lane, 0, trow);
+                    write_cstar<C>(sh, creg, sh.qrec[cur_buf], fx, 0, wave, ln, 0, trow);
                 }
 #pragma unroll 1
                 for (int j0 = wave * 4; j0 < nfx; j0 += 4 * NWL)
-                    a2_group<C, false>(sh, j0, nfx, sh.q[cur_buf], sh.qrec[cur_buf], 0, sh.fxl, lane);
+                    a2_group<C, false>(sh, j0, nfx, sh.q[cur_buf], sh.qrec[cur_buf], 0, sh.fxl, ln);
                 lds_barrier();
             }
         }
         STAMP(3)
         // ---- part 3: commit the valid prefix of the pending batch
+        ln = opaque_v(ln);
         int fj = -1;
         if (has_p) {
-            const uint64_t bad = __ballot(lane < P_n && sh.inval[lane] != 0);
+            const uint64_t bad = __ballot(ln < P_n && sh.inval[ln] != 0);
             fj = bad ? __ffsll((long long)bad) - 1 : -1;
         }
         if (wave == kErrWave && has_p) {
             // cluster ids, counts and the residual in query order (encoder.lpr:743:
             // err += sqrt(best / colCount)) -- beside wave 0's log update
             const int k = fj >= 0 ? fj : P_n;
-            const int j = lane;
+            const int j = ln;
             const bool cj = j < k;
             const QRecT<D>& R = sh.qrec[P_buf][P_off + (cj ? j : 0)];
             if (cj && wg0) {
                 clusters[P_s + P_off + j] = R.id;
                 atomicAdd(&cnta[R.cstar], 1);
             }
-            const float sq = cj ? __fsqrt_rn(sh.gp[j] / (float)D) : 0.0f;
+            const float sq = cj ? __fsqrt_rn(per_col(sh.gp[j])) : 0.0f;
 #pragma unroll
             for (int jj = 0; jj < KB; ++jj) {
                 const double t = (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(sq), jj));
@@ -1867,7 +1890,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         }
         if (wave == 0 && has_p) {
             const int k = fj >= 0 ? fj : P_n;
-            const int j = lane;
+            const int j = ln;
             const bool cj = j < k;
             const QRecT<D>& R = sh.qrec[P_buf][P_off + (cj ? j : 0)];
             // the last committed update of each centroid becomes its log entry:
@@ -1876,9 +1899,9 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             int tgt = lastc ? sh.ient[j] : -1;
             const uint64_t need = __ballot(lastc && tgt < 0);
             const uint64_t freem = __ballot(lg_pos < 0);
-            const uint64_t below = (1ull << lane) - 1ull;
-            sh.asg[lane] = -1;
-            if (lg_pos < 0) sh.freel[__popcll(freem & below)] = lane;
+            const uint64_t below = (1ull << ln) - 1ull;
+            sh.asg[ln] = -1;
+            if (lg_pos < 0) sh.freel[__popcll(freem & below)] = ln;
             wave_lds_sync();
             if (lastc && tgt < 0) tgt = sh.freel[__popcll(need & below)];
             if (lastc) {
@@ -1888,12 +1911,12 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 sh.asg[tgt] = R.cstar;
             }
             wave_lds_sync();
-            const int a = sh.asg[lane];
+            const int a = sh.asg[ln];
             if (a >= 0) {
                 lg_pos = a;
                 lg_tag = it;
             }
-            if (fj >= 0 && lane < D) sh.qslow[lane] = sh.q[P_buf][P_off + fj][lane];
+            if (fj >= 0 && ln < D) sh.qslow[ln] = sh.q[P_buf][P_off + fj][ln];
         }
         // queue bookkeeping (uniform)
         const int solo_j = fj >= 0 ? P_s + P_off + fj : -1;
@@ -1946,28 +1969,29 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         }
         if (wave == 0) {  // publish this iteration's commits (earlier ones are in the registers)
             const bool fresh_e = lg_pos >= 0 && lg_tag == it;
-            sh.pub_pos[lane] = fresh_e ? lg_pos : -1;
-            if (PRUNE && lane < KB) sh.ub[lane] = kInfBits;  // the next batch's bounds
+            sh.pub_pos[ln] = fresh_e ? lg_pos : -1;
+            if (PRUNE && ln < KB) sh.ub[ln] = kInfBits;  // the next batch's bounds
         }
         lds_barrier();
         STAMP(4)
         // ---- part 4: fold the log into the registers
-        refresh<C>(sh, creg, cn, cnmax, vwave, lane, trow);
+        ln = opaque_v(ln);
+        refresh<C>(sh, creg, cn, cnmax, vwave, ln, trow);
         if (solo_j >= 0) {
             // the failed query on the live centroids: fresh distances and
             // certificate; exact DFS if the certificate still fails
             ++restarts;
-            a1_query<C>(creg, sh.qslow, sh.wrec[vwave][KB], vwave, lane, dmask, trow, p0, tw_pass);
+            a1_query<C>(creg, sh.qslow, sh.wrec[vwave][KB], vwave, ln, dmask, trow, p0, tw_pass);
             lds_barrier();
             if constexpr (NWG == 2) {
-                write_cstar<C>(sh, creg, &sh.qsolo, 1ull, KB, wave, lane, wg);
+                write_cstar<C>(sh, creg, &sh.qsolo, 1ull, KB, wave, ln, wg);
                 lds_barrier();
                 xchg_records<C>(sh, xp, 1, nullptr, KB, &sh.qsolo, tid, wg);
                 lds_barrier();
             }
             if (wave == 0)
                 a2_group<C, false>(sh, 0, 1, reinterpret_cast<const float(*)[C::QD]>(sh.qslow), &sh.qsolo, KB,
-                                   nullptr, lane);
+                                   nullptr, ln);
             lds_barrier();
             int bpos;
             float key;
@@ -2022,7 +2046,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                     bpos = sh.slow_pos;
                     key = sh.slow_key;
                 } else {
-                    dfs_parallel<C>(sh, tid, lane, wave, bpos, key);
+                    dfs_parallel<C>(sh, tid, ln, wave, bpos, key);
                 }
                 bpos = uniform_int(bpos);
                 ++slow_total;
@@ -2055,9 +2079,9 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 }
             }
             lds_barrier();
-            if (wave == kErrWave && lane == 0) err += (double)__fsqrt_rn(key / (float)D);
+            if (wave == kErrWave && ln == 0) err += (double)__fsqrt_rn(per_col(key));
             if (wave == 0) {
-                if (lane == 0) {
+                if (ln == 0) {
                     const float rate = sh.rate[bpos];
                     for (int d = 0; d < D; ++d) {
                         const float o = sh.solo_c[d];
@@ -2071,17 +2095,17 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 wave_lds_sync();
                 const uint64_t hit = __ballot(lg_pos == bpos);
                 const int e = hit ? __ffsll((long long)hit) - 1 : __ffsll((long long)__ballot(lg_pos < 0)) - 1;
-                if (lane == e) {
+                if (ln == e) {
                     lg_pos = bpos;
                     lg_tag = it;
 #pragma unroll
                     for (int d = 0; d < D; ++d) sh.lg_c[e][d] = sh.solo_c[d];
                     sh.lg_c[e][C::ROW - 1] = half ? norm2_x<C::H>(sh.solo_c) : norm2_x<D>(sh.solo_c);
                 }
-                sh.pub_pos[lane] = lane == e ? bpos : -1;
+                sh.pub_pos[ln] = ln == e ? bpos : -1;
             }
             lds_barrier();
-            refresh<C>(sh, creg, cn, cnmax, vwave, lane, trow);
+            refresh<C>(sh, creg, cn, cnmax, vwave, ln, trow);
         }
         STAMP(5)
         if (nvq == 0 && cur_n == 0) {

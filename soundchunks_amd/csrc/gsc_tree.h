@@ -682,5 +682,15 @@ __device__ __forceinline__ T* uniform_ptr(T* p) {
     return (T*)(((uint64_t)hi << 32) | lo);
 }
 __device__ __forceinline__ int uniform_int(int v) { return __builtin_amdgcn_readfirstlane(v); }
+// a wave-uniform 64-bit offset (SGPRs).  Offset a kernel-argument pointer with
+// it instead of passing the sum through uniform_ptr: the integer round trip of
+// uniform_ptr hides the global address space, the compiler then emits FLAT
+// loads / stores, and every FLAT op also counts in lgkmcnt -- the next LDS wait
+// would wait for the HBM access too
+__device__ __forceinline__ int64_t uniform_i64(int64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
 
 }  // namespace gsc

@@ -105,6 +105,12 @@ CASES = {
     # KNNFit over 4N candidates; quiet input keeps <= 4096 entries after pruning
     "silence_burst_pr0_cs8": (lambda: _silence_burst(), ["-cs8", "-pr0"]),
     "quiet_tone_pr0_cs4": (lambda: _quiet_tone(seconds=2.0, frac=0.97), ["-cs4", "-pr0"]),
+    # any ChunkSize (-cs is unclamped, encoder.lpr:1992; odd sizes, decoder.lpr:151-156): 2*CS features
+    # padded with zeros to the 8 / 16 / 32-wide kernels (gsc_device.h feature_stride)
+    "syn3s_cs2_cpf512": (lambda: _synth(3.0), ["-cs2", "-cpf512"]),
+    "syn3s_cs3_mono_cbd12": (lambda: _synth(3.0, 44100, 1), ["-cs3", "-cpf1000", "-cbd12"]),
+    "syn3s_cs6_cpf1024_cbd12": (lambda: _synth(3.0), ["-cs6", "-cpf1024", "-cbd12"]),
+    "syn3s_cs12_cpf2048": (lambda: _synth(3.0), ["-cs12", "-cpf2048"]),
     # a frame of more than 262,144 chunks (13-s frames at 48 kHz stereo -cs4: N ~ 312,000): yakmo's
     # chosen-point bitmap and prefix summaries live in HBM instead of LDS
     "syn13s_48k_cs4_cpf256_fl13000": (lambda: _synth(13.0, 48000), ["-cs4", "-cpf256", "-fl13000"]),

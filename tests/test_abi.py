@@ -44,7 +44,7 @@ def test_library_exports_every_declared_symbol():
 
 ARGVS = [[], ["-cs8", "-cpf4096", "-cbd8"], ["-cs16", "-cpf4096", "-cbd12"], ["-cs8", "-cpf256"], ["-cpf100"],
          ["-cpf9999"], ["-cbd12", "-cb3", "-cs8"], ["-pr2", "-fl2500", "-vfr0.5"], ["-vfr3"], ["-pbb", "-v"],
-         ["-cs8", "-cb"], ["-br128"], ["-cbdx"]]
+         ["-cs8", "-cb"], ["-br128"], ["-cbdx"], ["-cs2"], ["-cs6", "-cbd12"], ["-cs12"], ["-cs17"], ["-cs0"]]
 
 
 @pytest.mark.parametrize("argv", ARGVS)
@@ -55,6 +55,23 @@ def test_option_parsing_matches_oracle(argv):
     p = oracle_ffi.params(argv)
     for f, _ in p._fields_:
         assert getattr(o, f) == getattr(p, f), (argv, f)
+
+
+@pytest.mark.parametrize("cs,ok", [(1, True), (3, True), (12, True), (16, True), (0, False), (17, False),
+                                   (32, False)])
+def test_chunk_size_range(cs, ok):
+    """-cs is unclamped in the reference (encoder.lpr:1992); the kernels take
+    2*ChunkSize <= 32 features, so ChunkSize 1..16 prepares and anything else is
+    refused up front (host code: no GPU needed)."""
+    import soundchunks_amd as sc
+    from soundchunks_amd.synth import synth_wav
+
+    enc = sc.Encoder([f"-cs{cs}"])
+    if ok:
+        assert enc.frame_count(synth_wav(5.0)) >= 1
+    else:
+        with pytest.raises(sc.GscError, match="ChunkSize"):
+            enc.frame_count(synth_wav(5.0))
 
 
 def test_no_gpu_fails_loudly():

@@ -2,7 +2,8 @@
 Build the stamps library first (make -C soundchunks_amd/csrc stamps), then:
     GSC_LIB=soundchunks_amd/lib/stamps/libsoundchunks_amd.so GSC_SCAN_DEBUG=1 \
         python tools/scan_stamps.py [passes] [cs]
-GSC_SCAN_LANE_LAYOUT=1 selects the VALU-only A1 layout."""
+(The batched kernel, scan_batch_kernel, is the only A1 layout: the MFMA one
+of round 2 was not kept)"""
 import os
 import sys
 import time
@@ -31,6 +32,6 @@ os.environ["GSC_SCAN_MAX_PASSES"] = str(passes)
 t = time.time()
 c, cl, it = sc.scan_reduce(feat, y, 3)
 dt = time.time() - t
-print(f"layout={'lane' if os.environ.get('GSC_SCAN_LANE_LAYOUT') else 'mfma'} N={feat.shape[0]} D={feat.shape[1]} "
+print(f"lib={os.environ.get('GSC_LIB', 'in-tree')} N={feat.shape[0]} D={feat.shape[1]} "
       f"passes={it} wall={dt:.3f}s us/search={dt / (it * feat.shape[0]) * 1e6:.3f} "
       f"crc={int(np.frombuffer(c.tobytes(), np.uint32).sum()) & 0xffffffff:08x}", flush=True)
