@@ -110,6 +110,9 @@ struct WaveRecT {     // A1 output per (wave, query): raw values of the argmin l
     int lanebits;     // L | 256 if another lane of the wave also holds the minimum
     uint32_t sl[6];   // lane L's sibling lane-group minima, groups of 2^b lanes (b = 0..5), as order keys
     uint32_t b[SL];   // lane L's SL leaf values (slots = kd leaves SL*L .. SL*L + SL-1 of the wave)
+    // (padding the record to an odd word count for conflict-free column reads
+    // was measured and not kept: 3827 vs 3713 ms, the single-lane record
+    // stores lose their 16-byte alignment)
 };
 
 // first slot of lane L at the wave minimum, and whether another slot ties it
@@ -169,8 +172,13 @@ struct Scan2Shared {
         float dist[kMaxK];
         WaveRecT<C::SL> wrec[C::NWV][C::KB + 1];  // column KB: the solo query
     };
+    // the records' minbits again, one word per (wave, column): lanes reading a
+    // column of wave minima (A2, write_cstar) hit distinct LDS banks, where the
+    // 16-word record stride is a 16-way conflict (written with every minbits)
+    uint32_t wmin[C::NWV][C::KB + 1];
     float rate[kMaxK];     // Single(1/sqrt(cnts[not Odd(iter)])) by kd-leaf position
     float dfs_inc[kMaxK];  // exact DFS: per split node box' increment, sign = near child hi
+    uint32_t dfs_near[kMaxK / 32];  // NaN passes' exact DFS: near child of split node h is low (bit h)
     alignas(16) float q[2][C::KB][C::QD];
     alignas(16) float qm[2][C::KB][C::QD];  // -2 q (exact), the A1 dot-product operand
     float cnmax[C::NWV];   // per (virtual) wave: upper bound of |c|^2 over its live centroids (monotone within a pass)
@@ -208,6 +216,10 @@ struct Scan2Shared {
     int asg[64];           // commit: log entry -> centroid position it now holds
     int slow_pos;
     float slow_key;
+    int vc_next;           // V check: next trip to take (reset in part 3)
+    int vps[5][64];        // wave 0's update-chain state (VPState) from vp_begin to vp_end, parked in LDS
+                           // (held in VGPRs across A1 it was spilled to scratch)
+    int vp_ready;          // V check: iteration + 1 whose update chain (vp_end) is complete
     int any_nan;
     int nan_rows;          // the pass has NaN centroids (yakmo 0/0 means): see nan_first below
     uint32_t nanid[kMaxK / 32];  // centroid id -> NaN row (fixed for the whole pass)
@@ -518,10 +530,11 @@ __device__ __forceinline__ A1Tree<C::SL> a1_tree(const float (&dv)[C::SL], int v
 }
 
 template <int SL>
-__device__ __forceinline__ void a1_store(const A1Tree<SL>& t, WaveRecT<SL>& rec, int lane) {
+__device__ __forceinline__ void a1_store(const A1Tree<SL>& t, WaveRecT<SL>& rec, uint32_t* wm, int lane) {
     const int L = __ffsll((long long)t.m) - 1;
     if (lane == L) {
         rec.minbits = t.lmin;
+        *wm = t.lmin;
         rec.lanebits = L | (__popcll(t.m) > 1 ? 256 : 0);
 #pragma unroll
         for (int i = 0; i < 6; ++i) rec.sl[i] = (uint32_t)t.sl[i];
@@ -531,19 +544,20 @@ __device__ __forceinline__ void a1_store(const A1Tree<SL>& t, WaveRecT<SL>& rec,
 }
 
 template <class C>
-__device__ __forceinline__ void a1_reduce(const float (&dv)[C::SL], WaveRecT<C::SL>& rec, int vwave, int lane) {
-    a1_store<C::SL>(a1_tree<C>(dv, vwave, lane), rec, lane);
+__device__ __forceinline__ void a1_reduce(const float (&dv)[C::SL], WaveRecT<C::SL>& rec, uint32_t* wm, int vwave,
+                                          int lane) {
+    a1_store<C::SL>(a1_tree<C>(dv, vwave, lane), rec, wm, lane);
 }
 
 // two queries: both DPP chains are computed before either record store, so
 // their latencies overlap
 template <class C>
 __device__ __forceinline__ void a1_reduce2(const float (&dv0)[C::SL], const float (&dv1)[C::SL], WaveRecT<C::SL>& rec0,
-                                           WaveRecT<C::SL>& rec1, int vwave, int lane) {
+                                           WaveRecT<C::SL>& rec1, uint32_t* wm0, uint32_t* wm1, int vwave, int lane) {
     const A1Tree<C::SL> t0 = a1_tree<C>(dv0, vwave, lane);
     const A1Tree<C::SL> t1 = a1_tree<C>(dv1, vwave, lane);
-    a1_store<C::SL>(t0, rec0, lane);
-    a1_store<C::SL>(t1, rec1, lane);
+    a1_store<C::SL>(t0, rec0, wm0, lane);
+    a1_store<C::SL>(t1, rec1, wm1, lane);
 }
 
 // max over the wave of a non-negative float (bit order = value order)
@@ -572,7 +586,7 @@ __device__ __forceinline__ float wave_min_nonneg(float x) {
 
 template <class C>
 __device__ __forceinline__ void a1_query(const float (&creg)[C::SL][C::DR], const float* __restrict__ qv,
-                                         WaveRecT<C::SL>& rec, int vwave, int lane, uint32_t dmask,
+                                         WaveRecT<C::SL>& rec, uint32_t* wm, int vwave, int lane, uint32_t dmask,
                                          const float* __restrict__ trow = nullptr, int p0 = 0, float tw = 0.0f) {
     float dv[C::SL];
     a1_dist<C::DR, C::SL>(creg, qv, dv);
@@ -601,7 +615,7 @@ __device__ __forceinline__ void a1_query(const float (&creg)[C::SL][C::DR], cons
     }
 #pragma unroll
     for (int s = 0; s < C::SL; ++s) dv[s] = ((dmask >> s) & 1u) ? __builtin_inff() : dv[s];  // padding leaves
-    a1_reduce<C>(dv, rec, vwave, lane);
+    a1_reduce<C>(dv, rec, wm, vwave, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -697,7 +711,7 @@ __device__ __forceinline__ void a2_group(Scan2Shared<C>& sh, int j0, int nq, con
     const int jj = jr;
     // global winner over the NW wave records (first wave at the minimum)
     const int wc = wcol0 + jr;
-    const uint32_t mw = (l < NW) ? sh.wrec[l][wc].minbits : kInfBits;
+    const uint32_t mw = (l < NW) ? sh.wmin[l][wc] : kInfBits;
     const uint32_t gmin = fmin16(mw);
     const uint32_t nmin = sum16((mw == gmin && l < NW) ? 1u : 0u);
     const int W = (int)min16((mw == gmin && l < NW) ? (uint32_t)l : 99u);
@@ -716,7 +730,7 @@ __device__ __forceinline__ void a2_group(Scan2Shared<C>& sh, int j0, int nq, con
         const int want = (W >> sh_) ^ 1;
 #pragma unroll
         for (int w = 0; w < NW; ++w)
-            if ((w >> sh_) == want) sib = fminb(sib, sh.wrec[w][wc].minbits);
+            if ((w >> sh_) == want) sib = fminb(sib, sh.wmin[w][wc]);
     } else if (l < LOGK) {
         // lane levels: depths [KW, LOGK - LS) -> sibling lane groups 5..0;
         // slot levels: depths [LOGK - LS, LOGK) -> 8 (quad), 7 (pair), 6 (slot)
@@ -927,20 +941,25 @@ __device__ __forceinline__ void vp_begin(Scan2Shared<C>& sh, int qb, int off, in
     for (uint32_t m = me; m; m &= m - 1u) atomicMin(&sh.vie[__ffs(m) - 1], lane);  // the entry holding c*_j
     wave_lds_sync();
     st.ie = lane < C::KB ? sh.vie[lane] : 64;
+    sh.vps[0][lane] = st.cs;  // parked for vp_end (VGPRs are scarce across A1)
+    sh.vps[1][lane] = st.pred;
+    sh.vps[2][lane] = st.nxt;
+    sh.vps[3][lane] = st.first;
+    sh.vps[4][lane] = st.ie;
 }
 
 template <class C>
-__device__ __forceinline__ void vp_end(Scan2Shared<C>& sh, int qb, int off, int pn, int lane, int lg_pos,
-                                       const VPState& st) {
+__device__ __forceinline__ void vp_end(Scan2Shared<C>& sh, int qb, int off, int pn, int lane, int lg_pos) {
     constexpr int D = C::D, KB = C::KB;
     const int j = lane;
     const bool act = j < pn;
     const QRecT<D>& R = sh.qrec[qb][off + (act ? j : 0)];
-    const int cs = st.cs, nxt = st.nxt;
-    const int ie = st.ie < 64 ? st.ie : -1;  // log entry holding c*_j (c*_j moved before the batch)
-    const int pred = st.pred >= 0 ? st.pred : ie;
+    const int cs = sh.vps[0][lane], nxt = sh.vps[2][lane], st_first = sh.vps[3][lane], st_ie = sh.vps[4][lane];
+    const int st_pred = sh.vps[1][lane];
+    const int ie = st_ie < 64 ? st_ie : -1;  // log entry holding c*_j (c*_j moved before the batch)
+    const int pred = st_pred >= 0 ? st_pred : ie;
     // versions: log entries (0..63) and "after query j" (64+j)
-    sh.vto[lane] = lg_pos >= 0 ? st.first : -1;
+    sh.vto[lane] = lg_pos >= 0 ? st_first : -1;
     if (lane < KB) {
         sh.vpos[64 + lane] = act ? cs : -1;
         sh.vfrom[64 + lane] = j + 1;
@@ -985,6 +1004,64 @@ __device__ __forceinline__ void vp_end(Scan2Shared<C>& sh, int qb, int off, int 
 template <class C>
 __device__ __forceinline__ void v_check_q(Scan2Shared<C>& sh, int qb, int off, int pn, int wave, int lane) {
     constexpr int D = C::D, KB = C::KB, QPL = 64 / KB, LOGK = C::LOGK;
+    constexpr int VSTEP = QPL * C::NWL;  // versions apart between this lane group's consecutive versions
+    const int j = lane % KB, grp = lane / KB;
+    const int jr = j < pn ? j : 0;
+    const QRecT<D>& R = sh.qrec[qb][off + jr];
+    const bool act = j < pn && R.pad_ == 0;  // a NaN-first answer holds whatever moved
+    const int cs = R.cstar;
+    const uint32_t fm = R.farmask;
+    const float g = sh.gp[jr];
+    float q[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) q[d] = sh.q[qb][off + jr][d];
+    bool bad = false;
+    // two versions per trip, every LDS read of a trip issued before its
+    // arithmetic (metadata, both rows and the certificate thresholds B[lca]):
+    // one round trip of latency per two versions instead of three per version
+#pragma unroll 1
+    for (int v0 = wave * QPL + grp; v0 < C::KVER; v0 += 2 * VSTEP) {
+        const int v1 = v0 + VSTEP < C::KVER ? v0 + VSTEP : v0;
+        const bool h1 = v0 + VSTEP < C::KVER;
+        const int vp0 = sh.vpos[v0], vp1 = h1 ? sh.vpos[v1] : -1;
+        const bool u0 = vp0 >= 0 && act && j >= sh.vfrom[v0] && j <= sh.vto[v0] && vp0 != cs;
+        const bool u1 = vp1 >= 0 && act && j >= sh.vfrom[v1] && j <= sh.vto[v1] && vp1 != cs;
+        if (!(u0 || u1)) continue;
+        const float* c0 = v0 < 64 ? sh.lg_c[v0] : sh.newc[v0 - 64];
+        const float* c1 = v1 < 64 ? sh.lg_c[v1] : sh.newc[v1 - 64];
+        const int lca0 = __clz(vp0 ^ cs) - (32 - LOGK), lca1 = __clz(vp1 ^ cs) - (32 - LOGK);
+        const float b0 = R.B[lca0 & 15], b1 = R.B[lca1 & 15];  // in range whatever lca is; used only when u
+        float du0 = 0.0f, du1 = 0.0f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const float t0 = fsub(q[d], c0[d]), t1 = fsub(q[d], c1[d]);
+            du0 = fadd(du0, fmul(t0, t0));
+            du1 = fadd(du1, fmul(t1, t1));
+        }
+        const bool far0 = (fm >> (lca0 & 31)) & 1u, far1 = (fm >> (lca1 & 31)) & 1u;
+        if (u0 && !(du0 > g && (!far0 || du0 > b0))) bad = true;
+        if (u1 && !(du1 > g && (!far1 || du1 > b1))) bad = true;
+    }
+    if (bad) sh.inval[j] = 1;
+}
+
+// The same checks as work items taken by whichever wave is free (one-CU
+// frames).  A1 is uneven across waves -- pruning leaves some waves a third of
+// the queries of others -- so the waves that finish A1 first run the V check
+// while the others still compute distances, instead of every wave doing an
+// eighth of it after the A1 barrier.  A trip = two versions per lane group
+// (as in v_check_q); the next trip's index is taken at the start of a trip
+// (LDS atomic), and the checks start once wave 0's update chain (vp_end) of
+// this iteration is published (vp_ready).
+template <class C>
+__device__ __forceinline__ void v_check_grab(Scan2Shared<C>& sh, int qb, int off, int pn, int lane) {
+    constexpr int D = C::D, KB = C::KB, QPL = 64 / KB, LOGK = C::LOGK;
+    constexpr int VPT = 2 * QPL;  // versions per trip
+    constexpr int NTRIP = (C::KVER + VPT - 1) / VPT;
+    int t = 0;
+    if (lane == 0) t = atomicAdd(&sh.vc_next, 1);
+    t = __builtin_amdgcn_readfirstlane(t);
+    if (t >= NTRIP) return;
     const int j = lane % KB, grp = lane / KB;
     const int jr = j < pn ? j : 0;
     const QRecT<D>& R = sh.qrec[qb][off + jr];
@@ -997,19 +1074,32 @@ __device__ __forceinline__ void v_check_q(Scan2Shared<C>& sh, int qb, int off, i
     for (int d = 0; d < D; ++d) q[d] = sh.q[qb][off + jr][d];
     bool bad = false;
 #pragma unroll 1
-    for (int v = wave * QPL + grp; v < C::KVER; v += QPL * C::NWL) {
-        const int vp = sh.vpos[v];
-        if (vp < 0 || !act || j < sh.vfrom[v] || j > sh.vto[v] || vp == cs) continue;
-        const float* c = v < 64 ? sh.lg_c[v] : sh.newc[v - 64];
-        float du = 0.0f;
+    while (t < NTRIP) {
+        int tn = 0;
+        if (lane == 0) tn = atomicAdd(&sh.vc_next, 1);  // the next trip, in flight during this one
+        const int v0 = t * VPT + 2 * grp;
+        const bool h0 = v0 < C::KVER, h1 = v0 + 1 < C::KVER;
+        const int v0s = h0 ? v0 : 0, v1 = h1 ? v0 + 1 : v0s;
+        const int vp0 = h0 ? sh.vpos[v0s] : -1, vp1 = h1 ? sh.vpos[v1] : -1;
+        const bool u0 = vp0 >= 0 && act && j >= sh.vfrom[v0s] && j <= sh.vto[v0s] && vp0 != cs;
+        const bool u1 = vp1 >= 0 && act && j >= sh.vfrom[v1] && j <= sh.vto[v1] && vp1 != cs;
+        if (u0 || u1) {
+            const float* c0 = v0s < 64 ? sh.lg_c[v0s] : sh.newc[v0s - 64];
+            const float* c1 = v1 < 64 ? sh.lg_c[v1] : sh.newc[v1 - 64];
+            const int lca0 = __clz(vp0 ^ cs) - (32 - LOGK), lca1 = __clz(vp1 ^ cs) - (32 - LOGK);
+            const float b0 = R.B[lca0 & 15], b1 = R.B[lca1 & 15];
+            float du0 = 0.0f, du1 = 0.0f;
 #pragma unroll
-        for (int d = 0; d < D; ++d) {
-            const float t = fsub(q[d], c[d]);
-            du = fadd(du, fmul(t, t));
+            for (int d = 0; d < D; ++d) {
+                const float t0 = fsub(q[d], c0[d]), t1 = fsub(q[d], c1[d]);
+                du0 = fadd(du0, fmul(t0, t0));
+                du1 = fadd(du1, fmul(t1, t1));
+            }
+            const bool far0 = (fm >> (lca0 & 31)) & 1u, far1 = (fm >> (lca1 & 31)) & 1u;
+            if (u0 && !(du0 > g && (!far0 || du0 > b0))) bad = true;
+            if (u1 && !(du1 > g && (!far1 || du1 > b1))) bad = true;
         }
-        const int lca = __clz(vp ^ cs) - (32 - LOGK);
-        const bool farl = (fm >> lca) & 1u;
-        if (!(du > g && (!farl || du > R.B[lca]))) bad = true;
+        t = __builtin_amdgcn_readfirstlane(tn);
     }
     if (bad) sh.inval[j] = 1;
 }
@@ -1128,123 +1218,172 @@ __device__ __forceinline__ void dfs_parallel(Scan2Shared<C>& sh, int tid, int la
     out_key = b;
 }
 
-// ANN's k = 1 search (annkSearch @0x1800124b0) over the stale tree with the
-// live distances in sh.dist, one lane, the recursion stack in LDS (dfs_inc,
-// free in passes that take this path): the NaN passes' exact DFS.  Their NaN
-// leaves carry +inf (inert: the query's descent reached a real leaf first), so
-// no leaf early exit changes a result; box' is tested at every far step, in
-// ANN's order, whatever its sign.  Same walk as scan_exact_dfs (gsc_tree.h),
-// kept in registers + LDS so the kernel's register block is not spilled
-// around a call.
+// Exact ANN search of the NaN passes, all threads.  NaN cut values and the
+// cells below them (bounds that contradict the cuts) make box' increments of
+// any sign, or NaN, so box' need not grow along a path and dfs_parallel's
+// one test on the innermost far subtree is not enough.  The rank argument
+// still holds: with the current best b found at DFS rank pos, a later leaf is
+// reached before the next improvement iff every far subtree on its path that
+// STARTS after pos has box' < b -- those are tested with b, the ones starting
+// before pos contain pos and were entered -- and starts grow with depth, so
+// that is a suffix of the path's far steps.  Each improvement round walks the
+// paths of the thread's 8 leaves (the first LOGK-3 levels shared) and takes
+// the suffix maximum of box' (NaN = +inf: never entered, ANN's `box' < key`
+// is false); the next improvement is the lowest-ranked reached leaf with
+// d < b (one block min-reduction per improvement, as in dfs_parallel).  NaN
+// and dead leaves carry +inf in sh.dist and never improve.  Same answers as
+// ANN's sequential walk (annkSearch @0x1800124b0; the oracle's ann_oracle.c).
 template <class C>
-__device__ __forceinline__ void dfs_exact_lds(Scan2Shared<C>& sh, int& out_pos, float& out_key) {
-    constexpr int D = C::D, K = C::K;
-    int* st_h = reinterpret_cast<int*>(sh.dfs_inc);
-    int* st_s = st_h + 16;
-    int* st_n = st_h + 32;
-    float* st_box = sh.dfs_inc + 48;
+__device__ __noinline__ void dfs_parallel_nan(Scan2Shared<C>& sh, int tid, int lane, int wave, int& out_pos,
+                                                 float& out_key) {
+    constexpr int D = C::D, LOGK = C::LOGK, NW = C::NWL;
+    constexpr int K = 1 << LOGK;
+    constexpr int nthreads = 64 * NW;
     const float* q = sh.qslow;
-    float cur_box = 0.0f;
+    for (int h0 = 0; h0 < K; h0 += nthreads) {  // split nodes: signed box' increment, near child
+        const int h = h0 + tid;
+        bool nearlo = false;
+        if (h < K - 1) {
+            const float qc = q[sh.t.cd[h]];
+            const float cut = fsub(qc, sh.t.cv[h]);
+            nearlo = cut < 0.0f;
+            float bd = nearlo ? fsub(sh.t.lo[h], qc) : fsub(qc, sh.t.hi[h]);
+            if (bd < 0.0f) bd = 0.0f;
+            sh.dfs_inc[h] = fsub(fmul(cut, cut), fmul(bd, bd));  // any sign, or NaN
+        }
+        const uint64_t m = __ballot(nearlo);  // 64 consecutive nodes per wave
+        if (lane == 0) {
+            sh.dfs_near[(h0 + wave * 64) >> 5] = (uint32_t)m;
+            sh.dfs_near[((h0 + wave * 64) >> 5) + 1] = (uint32_t)(m >> 32);
+        }
+    }
+    float rootbox = 0.0f;
+#pragma unroll
     for (int d = 0; d < D; ++d) {  // annBoxDistance
         const float qd = q[d];
-        if (qd < sh.t.bnd_lo[d]) {
+        if (sh.t.bnd_lo[d] > qd) {
             const float t = fsub(sh.t.bnd_lo[d], qd);
-            cur_box = fadd(cur_box, fmul(t, t));
+            rootbox = fadd(rootbox, fmul(t, t));
         } else if (qd > sh.t.bnd_hi[d]) {
             const float t = fsub(qd, sh.t.bnd_hi[d]);
-            cur_box = fadd(cur_box, fmul(t, t));
+            rootbox = fadd(rootbox, fmul(t, t));
         }
     }
-    int sp = 0, best = -1, h = 0, s = 0, n = K;
-    float key = FLT_MAX;  // max_key of the empty list (ANN_DIST_INF)
+    lds_barrier();
+    const int p0 = tid * 8;
+    auto far_step = [&](int h, int bit, int l, float& box, float& M, int& pref, int pos) {
+        const int nearbit = ((sh.dfs_near[h >> 5] >> (h & 31)) & 1u) ? 0 : 1;
+        if (bit != nearbit) {  // the leaf lies in the far child: its subtree starts after the near one
+            box = fadd(box, sh.dfs_inc[h]);
+            pref += 1 << (LOGK - 1 - l);
+            if (pref > pos) M = box != box ? __builtin_inff() : fmaxf(M, box);
+        }
+    };
+    int pos = -1, bp = -1, par = 0;
+    float b = FLT_MAX;  // the empty list's max_key
     for (;;) {
-        if (n == 1) {
-            const float dd = sh.dist[s];
-            if (!(dd > key) && (best < 0 || key > dd)) {  // ANNkd_leaf::ann_search + ANNmin_k::insert
-                key = dd;
-                best = s;
-            }
-            bool found = false;
-            while (sp > 0) {  // back up: the far child is visited iff box' < max_key
-                --sp;
-                if (st_box[sp] < key) {
-                    h = st_h[sp];
-                    s = st_s[sp];
-                    n = st_n[sp];
-                    cur_box = st_box[sp];
-                    found = true;
-                    break;
-                }
-            }
-            if (!found) break;
-            continue;
+        float box = rootbox, M = -__builtin_inff();
+        int pref = 0, h = 0;
+        for (int l = 0; l < LOGK - 3; ++l) {
+            const int bit = (p0 >> (LOGK - 1 - l)) & 1;
+            far_step(h, bit, l, box, M, pref, pos);
+            h = 2 * h + 1 + bit;
         }
-        const int half = n >> 1;
-        const float qc = q[sh.t.cd[h]];
-        const float cut = fsub(qc, sh.t.cv[h]);
-        float bd;
-        if (cut < 0.0f) {  // ANNkd_split::ann_search: near child first, far child + box' stacked
-            bd = fsub(sh.t.lo[h], qc);
-            st_h[sp] = 2 * h + 2;
-            st_s[sp] = s + half;
-            st_n[sp] = n - half;
-            h = 2 * h + 1;
-            n = half;
-        } else {
-            bd = fsub(qc, sh.t.hi[h]);
-            st_h[sp] = 2 * h + 1;
-            st_s[sp] = s;
-            st_n[sp] = half;
-            h = 2 * h + 2;
-            s += half;
-            n -= half;
+        uint32_t key = 0xFFFFFFFFu;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            float box2 = box, M2 = M;
+            int pref2 = pref, h2 = h;
+#pragma unroll
+            for (int l = LOGK - 3; l < LOGK; ++l) {
+                const int bit = ((p0 + s) >> (LOGK - 1 - l)) & 1;
+                far_step(h2, bit, l, box2, M2, pref2, pos);
+                h2 = 2 * h2 + 1 + bit;
+            }
+            if (p0 + s < K && pref2 > pos && M2 < b && sh.dist[p0 + s] < b)
+                key = min(key, ((uint32_t)pref2 << 12) | (uint32_t)(p0 + s));
         }
-        if (bd < 0.0f) bd = 0.0f;
-        st_box[sp] = fadd(cur_box, fsub(fmul(cut, cut), fmul(bd, bd)));
-        ++sp;
+        key = min(key, partner<0>(key));
+        key = min(key, partner<1>(key));
+        key = min(key, partner<2>(key));
+        key = min(key, partner<3>(key));
+        key = min(key, partner<4>(key));
+        key = min((uint32_t)__builtin_amdgcn_readlane((int)key, 0), (uint32_t)__builtin_amdgcn_readlane((int)key, 32));
+        if (lane == 0) sh.wkey[par][wave] = key;
+        lds_barrier();
+        uint32_t g = 0xFFFFFFFFu;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) g = min(g, sh.wkey[par][w]);
+        par ^= 1;
+        if (g == 0xFFFFFFFFu) break;
+        pos = (int)(g >> 12);
+        bp = (int)(g & 4095u);
+        b = sh.dist[bp];
     }
-    out_pos = best;
-    out_key = key;
+    out_pos = bp;
+    out_key = b;
 }
 
-// fold published log entries into the owners' registers
+// fold published log entries into the owners' registers: two entries per
+// trip (both rows read before either is applied), the pruning box and the
+// norm bound accumulated in registers and written once
 template <class C>
 __device__ __forceinline__ void refresh(Scan2Shared<C>& sh, float (&creg)[C::SL][C::DR], float (&cn)[C::SL],
                                         float& cnmax, int vwave, int lane, float* __restrict__ trow = nullptr) {
-    constexpr int SL = C::SL, LS = C::LS, D = C::D;
+    constexpr int SL = C::SL, LS = C::LS, D = C::D, DR = C::DR;
     const int pp = sh.pub_pos[lane];
     uint64_t m = __ballot(pp >= 0 && (pp >> (6 + LS)) == vwave);
-    const bool any = m != 0;
-    while (m) {
-        const int e = __ffsll((long long)m) - 1;
-        m &= m - 1;
-        const int p = __builtin_amdgcn_readlane(pp, e);
+    if (!m) return;
+    float blo = __builtin_inff(), bhi = -__builtin_inff();  // lane d < D: the new positions' range
+    auto apply = [&](int e, int p, const float* r, float nv) {
         const int owner = (p >> LS) & 63, slot = p & (SL - 1);
-        const float nv = sh.lg_c[e][C::ROW - 1];  // |c|^2, written with the entry
-        // the wave's norm bound only grows within a pass (A2 reads it for any earlier snapshot)
-        cnmax = fmaxf(cnmax, nv);
-        if (C::NWG == 1 && lane < D) {  // the pruning box covers the new position
-            const float v = sh.lg_c[e][lane];
-            sh.wlo[vwave][lane] = fminf(sh.wlo[vwave][lane], v);
-            sh.whi[vwave][lane] = fmaxf(sh.whi[vwave][lane], v);
-        }
 #pragma unroll
         for (int s = 0; s < SL; ++s) {
             if (s == slot) {
 #pragma unroll
-                for (int d = 0; d < C::DR; ++d) {
-                    const float v = sh.lg_c[e][d];
-                    creg[s][d] = lane == owner ? v : creg[s][d];
-                }
+                for (int d = 0; d < DR; ++d) creg[s][d] = lane == owner ? r[d] : creg[s][d];
                 cn[s] = lane == owner ? nv : cn[s];
             }
         }
         if constexpr (C::SPLIT) {  // the owner's tail row (only the owner lane ever reads it)
             if (lane == owner)
-                for (int d = C::DR; d < D; ++d) trow[(int64_t)p * C::TL + (d - C::DR)] = sh.lg_c[e][d];
+                for (int d = DR; d < D; ++d) trow[(int64_t)p * C::TL + (d - DR)] = sh.lg_c[e][d];
+        }
+    };
+    // two entries per trip where the second row fits the register budget (D = 8;
+    // at D = 16 the extra 16 VGPRs cost 40 spilled registers elsewhere)
+    constexpr bool PAIR = DR <= 8;
+    while (m) {
+        const int e0 = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const bool two = PAIR && m != 0;
+        const int e1 = two ? __ffsll((long long)m) - 1 : e0;
+        if (two) m &= m - 1;
+        const int p0 = __builtin_amdgcn_readlane(pp, e0), p1 = __builtin_amdgcn_readlane(pp, e1);
+        float r0[DR], r1[PAIR ? DR : 1];
+#pragma unroll
+        for (int d = 0; d < DR; ++d) {
+            r0[d] = sh.lg_c[e0][d];
+            if constexpr (PAIR) r1[d] = sh.lg_c[e1][d];
+        }
+        const float nv0 = sh.lg_c[e0][C::ROW - 1], nv1 = sh.lg_c[e1][C::ROW - 1];  // |c|^2, written with the entry
+        if (C::NWG == 1 && lane < D) {  // the pruning box covers the new positions
+            const float v0 = sh.lg_c[e0][lane], v1 = sh.lg_c[e1][lane];
+            blo = fminf(blo, fminf(v0, v1));
+            bhi = fmaxf(bhi, fmaxf(v0, v1));
+        }
+        // the wave's norm bound only grows within a pass (A2 reads it for any earlier snapshot)
+        cnmax = fmaxf(cnmax, fmaxf(nv0, nv1));
+        apply(e0, p0, r0, nv0);
+        if constexpr (PAIR) {
+            if (two) apply(e1, p1, r1, nv1);
         }
     }
-    if (any && lane == 0) sh.cnmax[vwave] = cnmax;
+    if (C::NWG == 1 && lane < D) {
+        sh.wlo[vwave][lane] = fminf(sh.wlo[vwave][lane], blo);
+        sh.whi[vwave][lane] = fmaxf(sh.whi[vwave][lane], bhi);
+    }
+    if (lane == 0) sh.cnmax[vwave] = cnmax;
 }
 
 // c*'s snapshot coordinates for the queries in qmask (columns col0 + j),
@@ -1268,7 +1407,7 @@ __device__ __forceinline__ void write_cstar(Scan2Shared<C>& sh, const float (&cr
         int W = 0;
 #pragma unroll
         for (int w = 0; w < NWL; ++w) {
-            const float m = __uint_as_float(sh.wrec[wg * NWL + w][col0 + jq].minbits);
+            const float m = __uint_as_float(sh.wmin[wg * NWL + w][col0 + jq]);
             if (m < gm) {
                 gm = m;
                 W = w;
@@ -1354,7 +1493,7 @@ __device__ __forceinline__ void xchg_records(Scan2Shared<C>& sh, XPort& x, int n
             const int jq = i / PQ, f = i - jq * PQ;
             const int col = cols ? col0 + cols[jq] : col0 + jq;
             if (f < NWL) {
-                sh.wrec[their0 + f][col].minbits = xget(x, i);
+                sh.wrec[their0 + f][col].minbits = sh.wmin[their0 + f][col] = xget(x, i);
             } else if (f == NWL) {
                 (void)xget(x, i);
             } else if (f < NWL + 1 + RW) {
@@ -1622,6 +1761,10 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         wave_box_init<C>(sh, creg, vwave, lane, p0, dmask);
         if (tid < KB) sh.ub[tid] = kInfBits;
     }
+    if (tid == 0) {  // V check work list: iteration tags start at 1 in every pass
+        sh.vc_next = 0;
+        sh.vp_ready = 0;
+    }
     // first batch's queries
     const int n0 = min(KB, N);
     for (int k = tid; k < n0 * D; k += nthreads) {
@@ -1743,7 +1886,8 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                     a1_dist_x2<C::H, C::DR, SL>(creg, cn, sh.qm[cur_buf][j0], sh.qm[cur_buf][j1], dv0, dv1);
                 else if constexpr (!C::SPLIT)
                     a1_dist_x2<D, D, SL>(creg, cn, sh.qm[cur_buf][j0], sh.qm[cur_buf][j1], dv0, dv1);
-                a1_reduce2<C>(dv0, dv1, sh.wrec[vwave][j0], sh.wrec[vwave][j1], vwave, ln);
+                a1_reduce2<C>(dv0, dv1, sh.wrec[vwave][j0], sh.wrec[vwave][j1], &sh.wmin[vwave][j0],
+                              &sh.wmin[vwave][j1], vwave, ln);
             }
         };
         const uint64_t curm = cur_n > 0 ? (cur_n >= 64 ? ~0ull : (1ull << cur_n) - 1ull) : 0ull;
@@ -1782,13 +1926,26 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 acn[2] += __popcll(curm & ~home & ~prunedm);
 #endif
                 if ((prunedm >> ln) & 1ull)  // a lower bound of this wave's A1 values (see above)
-                    sh.wrec[vwave][ln].minbits = __float_as_uint(fsub(fsub(lbp, fmul(3.0f, eps_j)), qn_j));
+                    sh.wrec[vwave][ln].minbits = sh.wmin[vwave][ln] =
+                        __float_as_uint(fsub(fsub(lbp, fmul(3.0f, eps_j)), qn_j));
                 a1_mask(curm & ~home & ~prunedm);
             }
         } else {
             a1_mask(curm);
         }
-        if (wave == 0 && has_p) vp_end<C>(sh, P_buf, P_off, P_n, ln, lg_pos, vst);
+        if (wave == 0 && has_p) vp_end<C>(sh, P_buf, P_off, P_n, ln, lg_pos);
+        if constexpr (NWG == 1) {
+            if (has_p) {  // V check of the pending batch by the waves done with A1 (v_check_grab)
+                if (wave == 0) {
+                    wave_lds_sync();
+                    if (ln == 0) __hip_atomic_store(&sh.vp_ready, it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else {
+                    while (__hip_atomic_load(&sh.vp_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != it + 1)
+                        __builtin_amdgcn_s_sleep(1);
+                }
+                v_check_grab<C>(sh, P_buf, P_off, P_n, ln);
+            }
+        }
 #ifdef GSC_STAMPS
         acn[3] += 1;
         acn[5] += P_n;
@@ -1807,7 +1964,9 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         }
         // ---- part 2: check the pending batch; certificates of the current batch
         ln = opaque_v(ln);
-        if (has_p) v_check_q<C>(sh, P_buf, P_off, P_n, wave, ln);
+        if constexpr (NWG == 2) {
+            if (has_p) v_check_q<C>(sh, P_buf, P_off, P_n, wave, ln);
+        }
         STAMP(7)
         if (cur_n > 0) {
             // c*'s snapshot coordinates (and exact distance), written by the wave that owns c*
@@ -1841,9 +2000,10 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                     m &= m - 1;
                     if ((prunedm >> jj) & 1ull) {  // still provably far: the exact record's lower bound
                         const float lb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbp), jj));
-                        if (ln == 0) sh.wrec[vwave][jj].minbits = __float_as_uint(lb);
+                        if (ln == 0) sh.wrec[vwave][jj].minbits = sh.wmin[vwave][jj] = __float_as_uint(lb);
                     } else {
-                        a1_query<C>(creg, sh.q[cur_buf][jj], sh.wrec[vwave][jj], vwave, ln, dmask, trow, p0, tw_pass);
+                        a1_query<C>(creg, sh.q[cur_buf][jj], sh.wrec[vwave][jj], &sh.wmin[vwave][jj], vwave, ln,
+                                    dmask, trow, p0, tw_pass);
                     }
                 }
                 lds_barrier();
@@ -1967,6 +2127,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 }
             }
         }
+        if (tid == 0) sh.vc_next = 0;  // the next iteration's V check trips (taken after the A1 barrier)
         if (wave == 0) {  // publish this iteration's commits (earlier ones are in the registers)
             const bool fresh_e = lg_pos >= 0 && lg_tag == it;
             sh.pub_pos[ln] = fresh_e ? lg_pos : -1;
@@ -1981,7 +2142,8 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             // the failed query on the live centroids: fresh distances and
             // certificate; exact DFS if the certificate still fails
             ++restarts;
-            a1_query<C>(creg, sh.qslow, sh.wrec[vwave][KB], vwave, ln, dmask, trow, p0, tw_pass);
+            a1_query<C>(creg, sh.qslow, sh.wrec[vwave][KB], &sh.wmin[vwave][KB], vwave, ln, dmask, trow, p0,
+                        tw_pass);
             lds_barrier();
             if constexpr (NWG == 2) {
                 write_cstar<C>(sh, creg, &sh.qsolo, 1ull, KB, wave, ln, wg);
@@ -2041,10 +2203,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 if (nan_rows) {
                     // NaN leaves carry +inf here: inert, as the query's descent
                     // reaches a real leaf first (NaN-first queries never fail)
-                    if (tid == 0) dfs_exact_lds<C>(sh, sh.slow_pos, sh.slow_key);
-                    lds_barrier();
-                    bpos = sh.slow_pos;
-                    key = sh.slow_key;
+                    dfs_parallel_nan<C>(sh, tid, ln, wave, bpos, key);
                 } else {
                     dfs_parallel<C>(sh, tid, ln, wave, bpos, key);
                 }
