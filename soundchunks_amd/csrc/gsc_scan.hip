@@ -172,10 +172,6 @@ struct Scan2Shared {
         float dist[kMaxK];
         WaveRecT<C::SL> wrec[C::NWV][C::KB + 1];  // column KB: the solo query
     };
-    // the records' minbits again, one word per (wave, column): lanes reading a
-    // column of wave minima (A2, write_cstar) hit distinct LDS banks, where the
-    // 16-word record stride is a 16-way conflict (written with every minbits)
-    uint32_t wmin[C::NWV][C::KB + 1];
     float rate[kMaxK];     // Single(1/sqrt(cnts[not Odd(iter)])) by kd-leaf position
     float dfs_inc[kMaxK];  // exact DFS: per split node box' increment, sign = near child hi
     uint32_t dfs_near[kMaxK / 32];  // NaN passes' exact DFS: near child of split node h is low (bit h)
@@ -217,8 +213,6 @@ struct Scan2Shared {
     int slow_pos;
     float slow_key;
     int vc_next;           // V check: next trip to take (reset in part 3)
-    int vps[5][64];        // wave 0's update-chain state (VPState) from vp_begin to vp_end, parked in LDS
-                           // (held in VGPRs across A1 it was spilled to scratch)
     int vp_ready;          // V check: iteration + 1 whose update chain (vp_end) is complete
     int any_nan;
     int nan_rows;          // the pass has NaN centroids (yakmo 0/0 means): see nan_first below
@@ -530,11 +524,10 @@ __device__ __forceinline__ A1Tree<C::SL> a1_tree(const float (&dv)[C::SL], int v
 }
 
 template <int SL>
-__device__ __forceinline__ void a1_store(const A1Tree<SL>& t, WaveRecT<SL>& rec, uint32_t* wm, int lane) {
+__device__ __forceinline__ void a1_store(const A1Tree<SL>& t, WaveRecT<SL>& rec, int lane) {
     const int L = __ffsll((long long)t.m) - 1;
     if (lane == L) {
         rec.minbits = t.lmin;
-        *wm = t.lmin;
         rec.lanebits = L | (__popcll(t.m) > 1 ? 256 : 0);
 #pragma unroll
         for (int i = 0; i < 6; ++i) rec.sl[i] = (uint32_t)t.sl[i];
@@ -544,20 +537,19 @@ __device__ __forceinline__ void a1_store(const A1Tree<SL>& t, WaveRecT<SL>& rec,
 }
 
 template <class C>
-__device__ __forceinline__ void a1_reduce(const float (&dv)[C::SL], WaveRecT<C::SL>& rec, uint32_t* wm, int vwave,
-                                          int lane) {
-    a1_store<C::SL>(a1_tree<C>(dv, vwave, lane), rec, wm, lane);
+__device__ __forceinline__ void a1_reduce(const float (&dv)[C::SL], WaveRecT<C::SL>& rec, int vwave, int lane) {
+    a1_store<C::SL>(a1_tree<C>(dv, vwave, lane), rec, lane);
 }
 
 // two queries: both DPP chains are computed before either record store, so
 // their latencies overlap
 template <class C>
 __device__ __forceinline__ void a1_reduce2(const float (&dv0)[C::SL], const float (&dv1)[C::SL], WaveRecT<C::SL>& rec0,
-                                           WaveRecT<C::SL>& rec1, uint32_t* wm0, uint32_t* wm1, int vwave, int lane) {
+                                           WaveRecT<C::SL>& rec1, int vwave, int lane) {
     const A1Tree<C::SL> t0 = a1_tree<C>(dv0, vwave, lane);
     const A1Tree<C::SL> t1 = a1_tree<C>(dv1, vwave, lane);
-    a1_store<C::SL>(t0, rec0, wm0, lane);
-    a1_store<C::SL>(t1, rec1, wm1, lane);
+    a1_store<C::SL>(t0, rec0, lane);
+    a1_store<C::SL>(t1, rec1, lane);
 }
 
 // max over the wave of a non-negative float (bit order = value order)
@@ -586,7 +578,7 @@ __device__ __forceinline__ float wave_min_nonneg(float x) {
 
 template <class C>
 __device__ __forceinline__ void a1_query(const float (&creg)[C::SL][C::DR], const float* __restrict__ qv,
-                                         WaveRecT<C::SL>& rec, uint32_t* wm, int vwave, int lane, uint32_t dmask,
+                                         WaveRecT<C::SL>& rec, int vwave, int lane, uint32_t dmask,
                                          const float* __restrict__ trow = nullptr, int p0 = 0, float tw = 0.0f) {
     float dv[C::SL];
     a1_dist<C::DR, C::SL>(creg, qv, dv);
@@ -615,7 +607,7 @@ __device__ __forceinline__ void a1_query(const float (&creg)[C::SL][C::DR], cons
     }
 #pragma unroll
     for (int s = 0; s < C::SL; ++s) dv[s] = ((dmask >> s) & 1u) ? __builtin_inff() : dv[s];  // padding leaves
-    a1_reduce<C>(dv, rec, wm, vwave, lane);
+    a1_reduce<C>(dv, rec, vwave, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -711,7 +703,7 @@ __device__ __forceinline__ void a2_group(Scan2Shared<C>& sh, int j0, int nq, con
     const int jj = jr;
     // global winner over the NW wave records (first wave at the minimum)
     const int wc = wcol0 + jr;
-    const uint32_t mw = (l < NW) ? sh.wmin[l][wc] : kInfBits;
+    const uint32_t mw = (l < NW) ? sh.wrec[l][wc].minbits : kInfBits;
     const uint32_t gmin = fmin16(mw);
     const uint32_t nmin = sum16((mw == gmin && l < NW) ? 1u : 0u);
     const int W = (int)min16((mw == gmin && l < NW) ? (uint32_t)l : 99u);
@@ -730,7 +722,7 @@ __device__ __forceinline__ void a2_group(Scan2Shared<C>& sh, int j0, int nq, con
         const int want = (W >> sh_) ^ 1;
 #pragma unroll
         for (int w = 0; w < NW; ++w)
-            if ((w >> sh_) == want) sib = fminb(sib, sh.wmin[w][wc]);
+            if ((w >> sh_) == want) sib = fminb(sib, sh.wrec[w][wc].minbits);
     } else if (l < LOGK) {
         // lane levels: depths [KW, LOGK - LS) -> sibling lane groups 5..0;
         // slot levels: depths [LOGK - LS, LOGK) -> 8 (quad), 7 (pair), 6 (slot)
@@ -941,25 +933,20 @@ __device__ __forceinline__ void vp_begin(Scan2Shared<C>& sh, int qb, int off, in
     for (uint32_t m = me; m; m &= m - 1u) atomicMin(&sh.vie[__ffs(m) - 1], lane);  // the entry holding c*_j
     wave_lds_sync();
     st.ie = lane < C::KB ? sh.vie[lane] : 64;
-    sh.vps[0][lane] = st.cs;  // parked for vp_end (VGPRs are scarce across A1)
-    sh.vps[1][lane] = st.pred;
-    sh.vps[2][lane] = st.nxt;
-    sh.vps[3][lane] = st.first;
-    sh.vps[4][lane] = st.ie;
 }
 
 template <class C>
-__device__ __forceinline__ void vp_end(Scan2Shared<C>& sh, int qb, int off, int pn, int lane, int lg_pos) {
+__device__ __forceinline__ void vp_end(Scan2Shared<C>& sh, int qb, int off, int pn, int lane, int lg_pos,
+                                       const VPState& st) {
     constexpr int D = C::D, KB = C::KB;
     const int j = lane;
     const bool act = j < pn;
     const QRecT<D>& R = sh.qrec[qb][off + (act ? j : 0)];
-    const int cs = sh.vps[0][lane], nxt = sh.vps[2][lane], st_first = sh.vps[3][lane], st_ie = sh.vps[4][lane];
-    const int st_pred = sh.vps[1][lane];
-    const int ie = st_ie < 64 ? st_ie : -1;  // log entry holding c*_j (c*_j moved before the batch)
-    const int pred = st_pred >= 0 ? st_pred : ie;
+    const int cs = st.cs, nxt = st.nxt;
+    const int ie = st.ie < 64 ? st.ie : -1;  // log entry holding c*_j (c*_j moved before the batch)
+    const int pred = st.pred >= 0 ? st.pred : ie;
     // versions: log entries (0..63) and "after query j" (64+j)
-    sh.vto[lane] = lg_pos >= 0 ? st_first : -1;
+    sh.vto[lane] = lg_pos >= 0 ? st.first : -1;
     if (lane < KB) {
         sh.vpos[64 + lane] = act ? cs : -1;
         sh.vfrom[64 + lane] = j + 1;
@@ -1407,7 +1394,7 @@ __device__ __forceinline__ void write_cstar(Scan2Shared<C>& sh, const float (&cr
         int W = 0;
 #pragma unroll
         for (int w = 0; w < NWL; ++w) {
-            const float m = __uint_as_float(sh.wmin[wg * NWL + w][col0 + jq]);
+            const float m = __uint_as_float(sh.wrec[wg * NWL + w][col0 + jq].minbits);
             if (m < gm) {
                 gm = m;
                 W = w;
@@ -1493,7 +1480,7 @@ __device__ __forceinline__ void xchg_records(Scan2Shared<C>& sh, XPort& x, int n
             const int jq = i / PQ, f = i - jq * PQ;
             const int col = cols ? col0 + cols[jq] : col0 + jq;
             if (f < NWL) {
-                sh.wrec[their0 + f][col].minbits = sh.wmin[their0 + f][col] = xget(x, i);
+                sh.wrec[their0 + f][col].minbits = xget(x, i);
             } else if (f == NWL) {
                 (void)xget(x, i);
             } else if (f < NWL + 1 + RW) {
@@ -1886,8 +1873,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                     a1_dist_x2<C::H, C::DR, SL>(creg, cn, sh.qm[cur_buf][j0], sh.qm[cur_buf][j1], dv0, dv1);
                 else if constexpr (!C::SPLIT)
                     a1_dist_x2<D, D, SL>(creg, cn, sh.qm[cur_buf][j0], sh.qm[cur_buf][j1], dv0, dv1);
-                a1_reduce2<C>(dv0, dv1, sh.wrec[vwave][j0], sh.wrec[vwave][j1], &sh.wmin[vwave][j0],
-                              &sh.wmin[vwave][j1], vwave, ln);
+                a1_reduce2<C>(dv0, dv1, sh.wrec[vwave][j0], sh.wrec[vwave][j1], vwave, ln);
             }
         };
         const uint64_t curm = cur_n > 0 ? (cur_n >= 64 ? ~0ull : (1ull << cur_n) - 1ull) : 0ull;
@@ -1926,14 +1912,13 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 acn[2] += __popcll(curm & ~home & ~prunedm);
 #endif
                 if ((prunedm >> ln) & 1ull)  // a lower bound of this wave's A1 values (see above)
-                    sh.wrec[vwave][ln].minbits = sh.wmin[vwave][ln] =
-                        __float_as_uint(fsub(fsub(lbp, fmul(3.0f, eps_j)), qn_j));
+                    sh.wrec[vwave][ln].minbits = __float_as_uint(fsub(fsub(lbp, fmul(3.0f, eps_j)), qn_j));
                 a1_mask(curm & ~home & ~prunedm);
             }
         } else {
             a1_mask(curm);
         }
-        if (wave == 0 && has_p) vp_end<C>(sh, P_buf, P_off, P_n, ln, lg_pos);
+        if (wave == 0 && has_p) vp_end<C>(sh, P_buf, P_off, P_n, ln, lg_pos, vst);
         if constexpr (NWG == 1) {
             if (has_p) {  // V check of the pending batch by the waves done with A1 (v_check_grab)
                 if (wave == 0) {
@@ -2000,10 +1985,10 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                     m &= m - 1;
                     if ((prunedm >> jj) & 1ull) {  // still provably far: the exact record's lower bound
                         const float lb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbp), jj));
-                        if (ln == 0) sh.wrec[vwave][jj].minbits = sh.wmin[vwave][jj] = __float_as_uint(lb);
+                        if (ln == 0) sh.wrec[vwave][jj].minbits = __float_as_uint(lb);
                     } else {
-                        a1_query<C>(creg, sh.q[cur_buf][jj], sh.wrec[vwave][jj], &sh.wmin[vwave][jj], vwave, ln,
-                                    dmask, trow, p0, tw_pass);
+                        a1_query<C>(creg, sh.q[cur_buf][jj], sh.wrec[vwave][jj], vwave, ln, dmask, trow, p0,
+                                    tw_pass);
                     }
                 }
                 lds_barrier();
@@ -2142,8 +2127,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             // the failed query on the live centroids: fresh distances and
             // certificate; exact DFS if the certificate still fails
             ++restarts;
-            a1_query<C>(creg, sh.qslow, sh.wrec[vwave][KB], &sh.wmin[vwave][KB], vwave, ln, dmask, trow, p0,
-                        tw_pass);
+            a1_query<C>(creg, sh.qslow, sh.wrec[vwave][KB], vwave, ln, dmask, trow, p0, tw_pass);
             lds_barrier();
             if constexpr (NWG == 2) {
                 write_cstar<C>(sh, creg, &sh.qsolo, 1ull, KB, wave, ln, wg);
