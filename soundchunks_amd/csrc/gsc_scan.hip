@@ -2136,23 +2136,32 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             // the failed query on the live centroids: fresh distances and
             // certificate; exact DFS if the certificate still fails
             ++restarts;
-            a1_query<C>(creg, sh.qslow, sh.wrec[vwave][KB], vwave, ln, dmask, trow, p0, tw_pass);
-            lds_barrier();
-            if constexpr (NWG == 2) {
-                write_cstar<C>(sh, creg, &sh.qsolo, 1ull, KB, wave, ln, wg);
+            // a query whose exact certificate already failed on its snapshot
+            // (fixup, part 2) goes straight to the exact DFS: the live centroids
+            // differ from the snapshot only in the few moved since, and the DFS
+            // gives ANN's answer whether or not a new certificate would pass
+            // (41 % of the restarts on the C2 frame; the fresh A1 + A2 they skip
+            // cost about 10k cycles each)
+            const bool snap_failed = NWG == 1 && uniform_int(sh.qrec[P_buf][P_off + fj].valid) == 0;
+            if (!snap_failed) {
+                a1_query<C>(creg, sh.qslow, sh.wrec[vwave][KB], vwave, ln, dmask, trow, p0, tw_pass);
                 lds_barrier();
-                xchg_records<C>(sh, xp, 1, nullptr, KB, &sh.qsolo, tid, wg);
+                if constexpr (NWG == 2) {
+                    write_cstar<C>(sh, creg, &sh.qsolo, 1ull, KB, wave, ln, wg);
+                    lds_barrier();
+                    xchg_records<C>(sh, xp, 1, nullptr, KB, &sh.qsolo, tid, wg);
+                    lds_barrier();
+                }
+                if (wave == 0)
+                    a2_group<C, false>(sh, 0, 1, reinterpret_cast<const float(*)[C::QD]>(sh.qslow), &sh.qsolo, KB,
+                                       nullptr, ln);
                 lds_barrier();
             }
-            if (wave == 0)
-                a2_group<C, false>(sh, 0, 1, reinterpret_cast<const float(*)[C::QD]>(sh.qslow), &sh.qsolo, KB,
-                                   nullptr, ln);
-            lds_barrier();
             int bpos;
             float key;
             bool dfs = false;
             STAMP(10)
-            if (uniform_int(sh.qsolo.valid)) {
+            if (!snap_failed && uniform_int(sh.qsolo.valid)) {
                 bpos = uniform_int(sh.qsolo.cstar);
                 key = sh.qsolo.g;
             } else {
