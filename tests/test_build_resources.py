@@ -55,7 +55,8 @@ def test_scan_kernel_register_block_not_in_scratch(tmp_path):
     for k in ks:
         spills = int(k.get("vgpr_spill_count", 0))
         private = int(k.get("private_segment_fixed_size", 0))
-        # spill slots (4 B per VGPR) plus a small fixed frame (up to 168 B
-        # seen, D = 32 K = 2048); a demoted centroid block adds >= 256 B
-        # (K = 256 at D = 8) up to 512 B per lane
-        assert private <= 4 * spills + 192, (k["name"], spills, private)
+        # spill slots (4 B per VGPR) plus a small fixed frame (up to 204 B
+        # seen: D = 32 K = 4096 with the out-of-line exact DFS's call frame);
+        # a demoted centroid block adds >= 256 B (K = 256 at D = 8) up to
+        # 512 B per lane
+        assert private <= 4 * spills + 224, (k["name"], spills, private)
