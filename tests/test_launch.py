@@ -91,3 +91,29 @@ def test_two_rank_job_equals_single_encode():
     assert nfr >= 4 and 0 < rng0[1] < nfr
     assert whole == oracle_ffi.encode(_tone_lsb(6.0), argv, threads=4)
     assert per_file == [b"r0" + b"r1", b"r0r0" + b"r1r1"]
+
+
+def test_bench_frame_digest_check(tmp_path, monkeypatch):
+    """bench.py's bit-exactness check splits a rank's output by the per-frame
+    byte counts and compares SHA-256 digests of the frames the table lists
+    (host logic; the GPU test runs it on real output)."""
+    import hashlib
+    import importlib.util
+    import json
+
+    spec = importlib.util.spec_from_file_location("bench_mod", ROOT / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    frames = [b"frame-a" * 3, b"frame-bb", b"c" * 11]
+    table = {"c2:8": {"frames": 5, "per_frame": {"2": hashlib.sha256(frames[0]).hexdigest(),
+                                                 "4": hashlib.sha256(frames[2]).hexdigest()}}}
+    db = tmp_path / "d.json"
+    db.write_text(json.dumps(table))
+    monkeypatch.setattr(bench, "DIGESTS", db)
+    blob, sizes = b"".join(frames), [len(f) for f in frames]
+    assert bench.frame_digest_check("c2:8", 2, blob, sizes, 5) == (2, 0, 2)  # frames 2..4, 2 and 4 listed
+    bad = frames[0] + frames[1] + b"c" * 10 + b"x"
+    assert bench.frame_digest_check("c2:8", 2, bad, sizes, 5) == (2, 1, 2)
+    assert bench.frame_digest_check("c2:8", 2, blob, sizes, 6)[1] == 1  # another frame cut
+    assert bench.frame_digest_check("c2:9", 0, blob, sizes, 5) == (0, 0, 0)  # no digests: unchecked
+    assert bench.frame_digest_check("c2:8", 2, blob + b"!", sizes, 5)[1] == 1  # bytes past the frames
