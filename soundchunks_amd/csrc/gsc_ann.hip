@@ -480,11 +480,11 @@ __global__ __launch_bounds__(kOvBlock) void knnfit_ann_kernel(const Tree* __rest
     // entries whose sqrt(err / CS) is SameValue with the first one's
     const float csf = (float)t.dd;
     int b = mk.n > 0 ? mk.info[0] : -1;
-    const float s0 = mk.n > 0 ? __fsqrt_rn(mk.key[0] / csf) : 0.0f;
+    const float s0 = mk.n > 0 ? sqrt_rn(mk.key[0] / csf) : 0.0f;
     for (int i = 0; i < mk.n; ++i) {
         const int id = mk.info[i];
         if (id >= 0 && id <= b - 1) {
-            const float sj = __fsqrt_rn(mk.key[i] / csf);
+            const float sj = sqrt_rn(mk.key[i] / csf);
             const float dl = s0 > sj ? fs(s0, sj) : fs(sj, s0);
             if (dl <= job.eps) b = id;
         }

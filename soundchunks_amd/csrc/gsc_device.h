@@ -24,6 +24,13 @@ constexpr int kMaxChunkSize = 16;  // ChunkSize up to 16: 2*CS <= 32 features (-
 // the padded search is the reference's search on the real features.
 __host__ __device__ constexpr int feature_stride(int cs) { return 2 * cs <= 8 ? 8 : (2 * cs <= 16 ? 16 : 32); }
 
+// IEEE (correctly rounded) f32 sqrt, as the reference's SSE sqrtss.  HIP's
+// __fsqrt_rn is __ocml_native_sqrt_f32 -- a bare v_sqrt_f32, 1 ulp -- unless
+// OCML_BASIC_ROUNDED_OPERATIONS is defined; __builtin_sqrtf lowers to
+// v_sqrt_f32 plus the +-1 ulp fma correction.  One ulp flips KNNFit's
+// SameValue-within-eps ties (encoder.lpr:955-962) and ScanReduce's err sum.
+__device__ inline float sqrt_rn(float x) { return __builtin_sqrtf(x); }
+
 // One frame of TFrame.Reduce / KNNScanReduce work (encoder.lpr:785-913, 699-765).
 struct ReduceFrame {
     int64_t x_off;        // Dataset: N*D floats at X + x_off (row major)

@@ -405,7 +405,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_pass_kernel(ReduceFrame* __
             if (me) sh.cnta[bpos] += 1;
             if (tid == 0) {
                 clusters[i] = id;
-                err += (double)__fsqrt_rn(per_col(bkey));
+                err += (double)sqrt_rn(per_col(bkey));
             }
         }
     }
@@ -544,7 +544,7 @@ __global__ __launch_bounds__(256) void knnfit_kernel(FitFrame* __restrict__ fram
                     // f order: 4c+0 fwd, 4c+1 rev, 4c+2 neg fwd, 4c+3 neg rev
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
-                        const float s = __fsqrt_rn(e[k] / (float)CS);
+                        const float s = sqrt_rn(e[k] / (float)CS);
                         const float dlt = s0 > s ? fsub(s0, s) : fsub(s, s0);
                         if (dlt <= eps) {
                             if (best < 0) best = 4 * (c0 + c) + k;
@@ -555,7 +555,7 @@ __global__ __launch_bounds__(256) void knnfit_kernel(FitFrame* __restrict__ fram
             }
         }
         if (pass == 0) {
-            s0 = __fsqrt_rn(e0 / (float)CS);
+            s0 = sqrt_rn(e0 / (float)CS);
             // acceptance is monotone in e: e > CS (s0 + eps)^2 (1 + 2^-16) never qualifies
             const float t = s0 + eps;
             ehi = (float)CS * t * t * 1.0000153f;

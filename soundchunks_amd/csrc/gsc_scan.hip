@@ -2035,7 +2035,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 clusters[P_s + P_off + j] = R.id;
                 atomicAdd(&cnta[R.cstar], 1);
             }
-            const float sq = cj ? __fsqrt_rn(per_col(sh.gp[j])) : 0.0f;
+            const float sq = cj ? sqrt_rn(per_col(sh.gp[j])) : 0.0f;
 #pragma unroll
             for (int jj = 0; jj < KB; ++jj) {
                 const double t = (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(sq), jj));
@@ -2242,7 +2242,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 }
             }
             lds_barrier();
-            if (wave == kErrWave && ln == 0) err += (double)__fsqrt_rn(per_col(key));
+            if (wave == kErrWave && ln == 0) err += (double)sqrt_rn(per_col(key));
             if (wave == 0) {
                 if (ln == 0) {
                     const float rate = sh.rate[bpos];

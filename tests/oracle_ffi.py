@@ -227,6 +227,21 @@ def scan_reduce(x, c0, precision=3, max_passes=100):
     return c, cl, n
 
 
+def knnfit_assign(fwd, q, eps):
+    """KNNFit's candidate choice f = 4c + 2neg + rev per query over the four
+    variants (fwd, rev, -fwd, -rev) of every forward row."""
+    fwd = np.ascontiguousarray(fwd, dtype=np.float32)
+    q = np.ascontiguousarray(q, dtype=np.float32)
+    r, cs = fwd.shape
+    cand4 = np.empty((4 * r, cs), dtype=np.float32)
+    cand4[0::4], cand4[1::4], cand4[2::4], cand4[3::4] = fwd, fwd[:, ::-1], -fwd, -fwd[:, ::-1]
+    out = np.zeros(q.shape[0], dtype=np.int32)
+    fp = ctypes.POINTER(ctypes.c_float)
+    load().ora_knnfit_assign(4 * r, cs, cand4.ctypes.data_as(fp), q.shape[0], q.ctypes.data_as(fp),
+                             ctypes.c_float(eps), out.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+    return out
+
+
 def stats() -> dict:
     s = OraStats()
     load().ora_get_stats(ctypes.byref(s))

@@ -153,6 +153,59 @@ def test_knnfit_synthetic_ties(oracle, cs, r, n, eps, seed):
     np.testing.assert_array_equal(got, want)
 
 
+def _u32(*h):
+    return np.array(h, dtype=np.uint32).view(np.float32)
+
+
+def test_knnfit_eps_tie_needs_ieee_sqrt(oracle):
+    """Frame 7 of the C2 bench (1024 s synthetic): |sqrt(e1/8) - sqrt(e0/8)| lands
+    0.3 ulp below eps, so the reference keeps the smaller index 2 (chunk 0,
+    negated).  A 1-ulp sqrt (HIP's __fsqrt_rn is v_sqrt_f32) rounds s1 up,
+    misses the tie and keeps index 6."""
+    import soundchunks_amd as sc
+
+    fwd = np.stack([_u32(0x3d8be665, 0x3d8f274a, 0x3d503926, 0x3dbff4af, 0x3e12682f, 0x3e1408a1, 0x3e1dcb4f,
+                         0x3e467678),
+                    _u32(0x3d281020, 0x3d5c3871, 0x3d566cda, 0x3e0f6ede, 0x3e1254a9, 0x3e199326, 0x3dfefdfc,
+                         0x3e2af5ec)])
+    q = _u32(0xbd5ae1b6, 0xbd86810d, 0xbd95b12b, 0xbdfb71f7, 0xbe02d106, 0xbe012902, 0xbe1a3134, 0xbe2ec15e)[None]
+    eps = float(_u32(0x3a24b306)[0])
+    assert oracle.knnfit_assign(fwd, q, eps).tolist() == [2]
+    assert sc.knnfit_assign(fwd, q, eps).tolist() == [2]
+
+
+def test_knnfit_eps_boundary_sweep(oracle):
+    """eps one ulp below, at and above the exact f32 gap sqrt(e1/CS) - sqrt(e0/CS)
+    for random query / candidate pairs: the choice flips exactly where the
+    oracle's does."""
+    import soundchunks_amd as sc
+
+    rng = np.random.default_rng(77)
+    f32 = np.float32
+    flips = 0
+    for t in range(24):
+        cs = (4, 8, 16)[t % 3]
+        fwd = rng.uniform(-0.3, 0.3, size=(2, cs)).astype(np.float32)
+        q = (fwd[1] + rng.normal(0, 0.01, size=cs)).astype(np.float32)[None]
+        var = [v for c in fwd for v in (c, c[::-1], -c, -c[::-1])]  # f = 4c + 2neg + rev
+        s = []
+        for v in var:
+            e = f32(0)
+            for j in range(cs):  # sequential f32 distance, as ANN
+                d = f32(q[0, j] - v[j])
+                e = f32(e + f32(d * d))
+            s.append(f32(np.sqrt(f32(e / f32(cs)))))
+        assert min(s[4:]) < min(s[:4])  # the nearest is a variant of chunk 1
+        gap = f32(min(s[:4]) - min(s[4:]))
+        for eps in (np.nextafter(gap, f32(0)), gap, np.nextafter(gap, f32(1))):
+            want = oracle.knnfit_assign(fwd, q, float(eps))
+            got = sc.knnfit_assign(fwd, q, float(eps))
+            assert got.tolist() == want.tolist(), (t, float(eps))
+        flips += int(oracle.knnfit_assign(fwd, q, float(np.nextafter(gap, f32(0))))[0] !=
+                     oracle.knnfit_assign(fwd, q, float(gap))[0])
+    assert flips >= 20  # the sweep does sit on the decision boundary
+
+
 # C4: the reference's lame_test corpus (tests/golden/lame_test, copied from the
 # reference as data) at -cs8 -cpf4096; expected digests from the oracle
 # (tests/golden/make_corpus.py)
