@@ -202,7 +202,9 @@ def frame_digest_check(key: str, frame_begin: int, blob: bytes, sizes, frames_to
         h = want.get(str(frame_begin + i))
         if h is not None:
             checked += 1
-            bad += hashlib.sha256(blob[o:o + n]).hexdigest() != h
+            if hashlib.sha256(blob[o:o + n]).hexdigest() != h:
+                bad += 1
+                print(f"bench.py: frame {frame_begin + i} differs from the oracle digest", file=sys.stderr)
         o += n
     if o != len(blob):
         bad += 1
@@ -224,7 +226,7 @@ def oracle_ffi_first_frame_wav(wav: bytes, argv) -> bytes:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--seconds", type=float, default=1024.0,
                     help="audio seconds per GPU (weak) or in total (--strong); 1024 s = 256 frames of 4 s")
@@ -346,6 +348,9 @@ def main():
     # the length of the gathered file when every frame has a digest
     key = f"{args.config}:{total_seconds:g}"
     fb, blob, sizes = info["own"]
+    if os.environ.get("BENCH_DUMP"):  # diagnostic: this rank's bytes and per-frame sizes of the last step
+        Path(os.environ["BENCH_DUMP"] + f".r{rank}.gsc").write_bytes(blob)
+        Path(os.environ["BENCH_DUMP"] + f".r{rank}.json").write_text(json.dumps({"first": fb, "sizes": sizes}))
     checked, bad, listed = frame_digest_check(key, fb, blob, sizes, info["frames"])
     if dist is not None:
         t = torch.tensor([checked, bad], dtype=torch.int64, device=cdev)
