@@ -162,17 +162,22 @@ struct DevBuf {
     }
 };
 
-// stream-ordered device buffer (hipMallocAsync / hipFreeAsync on one stream)
+// stream-ordered device buffer (hipMallocAsync / hipFreeAsync on one stream);
+// on the null stream (the synchronous drop-in ABI calls) plain hipMalloc / hipFree
 template <typename T>
 struct StreamBuf {
     T* p = nullptr;
     hipStream_t st;
     explicit StreamBuf(hipStream_t s) : st(s) {}
     ~StreamBuf() {
-        if (p) (void)hipFreeAsync(p, st);
+        if (!p) return;
+        if (st) (void)hipFreeAsync(p, st);
+        else (void)hipFree(p);
     }
     hipError_t alloc(size_t count) {
-        return hipMallocAsync(reinterpret_cast<void**>(&p), sizeof(T) * std::max<size_t>(count, 1), st);
+        const size_t bytes = sizeof(T) * std::max<size_t>(count, 1);
+        if (!st) return hipMalloc(reinterpret_cast<void**>(&p), bytes);
+        return hipMallocAsync(reinterpret_cast<void**>(&p), bytes, st);
     }
 };
 
