@@ -63,7 +63,7 @@ CORPUS = ROOT / "tests" / "golden" / "lame_test"
 
 VALU_F32_PEAK_TOPS = 78.6  # non-fused f32 VALU ops/s: half the 157.3 TFLOPS FMA-counted peak
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md (spec)
-PMC_SUMMARY = ROOT / "profiles" / "r03" / "pmc_summary.json"  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
+PMC_SUMMARY = ROOT / "profiles" / "r04" / "pmc_summary.json"  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
 DIGESTS = ROOT / "tests" / "golden" / "bench_digests.json"  # oracle per-frame .gsc digests (make_bench_digests.py)
 CORPUS_META = ROOT / "tests" / "golden" / "corpus_meta.json"  # oracle .gsc digests of the lame_test files
 
