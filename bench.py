@@ -135,6 +135,15 @@ def cpu_baseline(cfg: str, argv, rate: int, channels: int, frame_seconds: float,
         sample = [synth_wav(frame_seconds * threads, rate, channels)]
     one_samples = (len(one_wav) - 44) // 2
     walls = [0.0] * runs
+    stop = threading.Event()
+    t_cpu = time.perf_counter()
+
+    def heartbeat():  # minutes of CPU work print nothing else: a progress line every 30 s
+        while not stop.wait(30.0):
+            print(f"bench.py: cpu_baseline running, {time.perf_counter() - t_cpu:.0f} s", file=sys.stderr, flush=True)
+
+    hb = threading.Thread(target=heartbeat, daemon=True)
+    hb.start()
 
     def run(i):
         t = time.perf_counter()
@@ -158,6 +167,8 @@ def cpu_baseline(cfg: str, argv, rate: int, channels: int, frame_seconds: float,
             with TP(threads) as pool:
                 list(pool.map(lambda w: oracle_ffi.encode(w, argv, threads=1), sample))
         wns.append(time.perf_counter() - t)
+    stop.set()
+    hb.join()
     wn = statistics.median(wns)
     nsamp = sum((len(w) - 44) // 2 for w in sample)
     allv = nsamp / wn / 1e6
