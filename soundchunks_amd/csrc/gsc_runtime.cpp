@@ -1795,10 +1795,11 @@ int gsc_scan_reduce(int n, int d0, const float* x, int k, float* centroids, int*
             std::fprintf(stderr, "\n  w%d:", w);
             for (int k = 0; k < 16; ++k) std::fprintf(stderr, " %.3g", double(fr[0].stamps[w * 16 + k]));
         }
-        std::fprintf(stderr, "\nA1 queries [home pruned evaluated | iterations fixups pending]");
+        std::fprintf(stderr, "\nA1 queries [home pruned evaluated | iterations fixups pending | clk: box+home midbarrier]"
+                             "\n  (one-CU frames: stamps slot 'vcheck' = A1 after the mid barrier + vp_end, slot 'A1' = the V check)");
         for (int w = 0; w < 8; ++w) {
             std::fprintf(stderr, "\n  w%d:", w);
-            for (int k = 0; k < 6; ++k) std::fprintf(stderr, " %.4g", double(fr[0].acounts[w * 8 + k]));
+            for (int k = 0; k < 8; ++k) std::fprintf(stderr, " %.4g", double(fr[0].acounts[w * 8 + k]));
         }
         std::fprintf(stderr, "\n");
     }

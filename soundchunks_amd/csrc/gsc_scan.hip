@@ -1911,7 +1911,18 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                     const float ubd = fmul(fadd(fadd(qn_j, m), eps_j), 1.0f + 0x1p-20f);
                     atomicMin(&sh.ub[ln], __float_as_uint(fmaxf(ubd, 0.0f)));
                 }
+#ifdef GSC_STAMPS
+                const uint64_t tm0_ = stamp();
+                acn[6] += tm0_ - tlast;  // box bounds + home queries
+#endif
                 lds_barrier();
+#ifdef GSC_STAMPS
+                {
+                    const uint64_t tm1_ = stamp();
+                    acn[7] += tm1_ - tm0_;  // the mid-A1 barrier
+                    tlast = tm1_;
+                }
+#endif
                 const float ubj = __uint_as_float(sh.ub[jr]);
                 const float thr = fmul(fadd(ubj, fmul(4.0f, eps_j)), 1.0f + 0x1p-20f);
                 prunedm = __ballot(lbp > thr) & curm & ~home;
@@ -1929,6 +1940,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         }
         if (wave == 0 && has_p) vp_end<C>(sh, P_buf, P_off, P_n, ln, lg_pos, vst);
         if constexpr (NWG == 1) {
+            STAMP(7)  // one-CU frames: slot 7 = the rest of A1 (+ vp_end); slot 1 = the V check below
             if (has_p) {  // V check of the pending batch by the waves done with A1 (v_check_grab)
                 if (wave == 0) {
                     wave_lds_sync();
@@ -1960,8 +1972,8 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         ln = opaque_v(ln);
         if constexpr (NWG == 2) {
             if (has_p) v_check_q<C>(sh, P_buf, P_off, P_n, wave, ln);
+            STAMP(7)
         }
-        STAMP(7)
         if (cur_n > 0) {
             // c*'s snapshot coordinates (and exact distance), written by the wave that owns c*
             if constexpr (NWG == 1)
