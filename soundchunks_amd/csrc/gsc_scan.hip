@@ -58,6 +58,10 @@
 
 namespace gsc {
 
+#ifndef GSC_EPSF8
+#define GSC_EPSF8 0x1p-18f  // A1 bound slack at D = 8 (< 56u of its 64u, see a1_dist_x2)
+#endif
+
 // Shape of one KNNScanReduce pipeline instance.
 template <int D_, int LOGK_, int SL_, int NWG_, int DR_ = D_>
 struct ScanCfg {
@@ -82,7 +86,7 @@ struct ScanCfg {
     static constexpr int H = D / 2;  // DCT half of the features; [H, D) = cepstrum x 1e-5 (encoder.lpr:1700-1716)
     static constexpr int ROW = D + 4;  // lane-indexed coordinate rows: 16-B multiple, odd x 16 B (no b128 conflicts)
     // A1 bound slack: eps(q) = (|q|^2 + M) * 2^-EPSX (see a1_dist_x2)
-    static constexpr float EPSF = D > 16 ? 0x1p-16f : 0x1p-17f;
+    static constexpr float EPSF = D > 16 ? 0x1p-16f : (D > 8 ? 0x1p-17f : GSC_EPSF8);
     static_assert(NWV <= 16, "A2 evaluates up to 16 wave records per query (one per lane of a 16-lane group)");
     static_assert(KB <= 32 && 64 % KB == 0, "batch size");
     static_assert(NWG == 1 || (FULL && NWL == 8), "two-CU frames: 8 full waves per workgroup");
@@ -199,9 +203,9 @@ struct Scan2Shared {
     double err_out;
     // commit of the pending batch: versions 0..63 = log entries, 64+j = after query j
     int vcs[C::KB];        // c* of the pending batch's queries (-2 past the batch)
-    int vpos[C::KVER];
-    int vfrom[C::KVER];    // first query that sees the version
-    int vto[C::KVER];      // last query that sees it
+    // per version: x = leaf position (-1 = none), y = first query that sees it,
+    // z = last query that sees it (one 16-B read per version in the V check)
+    alignas(16) int4 vmeta[C::KVER];
     alignas(16) float newc[C::KB][C::ROW];
     float gp[C::KB];       // live d(q_j, c*_j)
     int inval[C::KB];
@@ -620,7 +624,9 @@ __device__ __forceinline__ void a1_query(const float (&creg)[C::SL][C::DR], cons
 // |q|^2) (every partial sum is within 2(|c|^2 + |q|^2) by Cauchy-Schwarz), the
 // two norms <= D u each, the final add <= 2u, the reference's own sum <=
 // (D+1) u d <= 2(D+1) u (|c|^2 + |q|^2); u = 2^-24.  D = 16: < 104u against
-// the 128u of 2^-17; D = 32: < 200u against the 256u of 2^-16.  A2 certifies
+// the 128u of 2^-17; D = 32: < 200u against the 256u of 2^-16; D = 8: < 56u
+// against the 64u of 2^-18 (D = 8 used 2^-17 before round 4: the halved slack
+// sends fewer certificates to the exact fixup, C5 -cs4 scan -3 %).  A2 certifies
 // only with that margin; what it cannot decide is re-run exactly on the same
 // snapshot (fixup in part 2).  The committed distance g is always recomputed
 // exactly from c*'s coordinates (vp_end).
@@ -906,8 +912,8 @@ __device__ __forceinline__ void vp_begin(Scan2Shared<C>& sh, int qb, int off, in
     if (lg_pos >= 0 && lg_tag < a1) lg_pos = -1;  // committed before the batch's snapshot
     // a NaN-first query moves nothing: a key of its own, so it joins no chain and no log entry
     st.cs = lane < pn ? (sh.qrec[qb][off + lane].pad_ ? -100 - lane : sh.qrec[qb][off + lane].cstar) : -2;
-    sh.vpos[lane] = lg_pos;
-    sh.vfrom[lane] = 0;
+    sh.vmeta[lane].x = lg_pos;
+    sh.vmeta[lane].y = 0;
     if (lane < C::KB) sh.vcs[lane] = st.cs;
     // pairs (query, query with the same c*) and (log entry, query moving it) by
     // position masks in LDS: qm[p] = the batch's queries whose c* is leaf p.
@@ -946,11 +952,9 @@ __device__ __forceinline__ void vp_end(Scan2Shared<C>& sh, int qb, int off, int 
     const int ie = st.ie < 64 ? st.ie : -1;  // log entry holding c*_j (c*_j moved before the batch)
     const int pred = st.pred >= 0 ? st.pred : ie;
     // versions: log entries (0..63) and "after query j" (64+j)
-    sh.vto[lane] = lg_pos >= 0 ? st.first : -1;
+    sh.vmeta[lane].z = lg_pos >= 0 ? st.first : -1;
     if (lane < KB) {
-        sh.vpos[64 + lane] = act ? cs : -1;
-        sh.vfrom[64 + lane] = j + 1;
-        sh.vto[64 + lane] = act ? nxt : -1;
+        sh.vmeta[64 + lane] = make_int4(act ? cs : -1, j + 1, act ? nxt : -1, 0);
         sh.nxt[lane] = nxt;
         sh.ient[lane] = ie;
         sh.inval[lane] = 0;
@@ -1010,9 +1014,10 @@ __device__ __forceinline__ void v_check_q(Scan2Shared<C>& sh, int qb, int off, i
     for (int v0 = wave * QPL + grp; v0 < C::KVER; v0 += 2 * VSTEP) {
         const int v1 = v0 + VSTEP < C::KVER ? v0 + VSTEP : v0;
         const bool h1 = v0 + VSTEP < C::KVER;
-        const int vp0 = sh.vpos[v0], vp1 = h1 ? sh.vpos[v1] : -1;
-        const bool u0 = vp0 >= 0 && act && j >= sh.vfrom[v0] && j <= sh.vto[v0] && vp0 != cs;
-        const bool u1 = vp1 >= 0 && act && j >= sh.vfrom[v1] && j <= sh.vto[v1] && vp1 != cs;
+        const int4 m0 = sh.vmeta[v0], m1 = sh.vmeta[v1];
+        const int vp0 = m0.x, vp1 = h1 ? m1.x : -1;
+        const bool u0 = (vp0 >= 0) & act & (j >= m0.y) & (j <= m0.z) & (vp0 != cs);
+        const bool u1 = (vp1 >= 0) & act & (j >= m1.y) & (j <= m1.z) & (vp1 != cs);
         if (!(u0 || u1)) continue;
         const float* c0 = v0 < 64 ? sh.lg_c[v0] : sh.newc[v0 - 64];
         const float* c1 = v1 < 64 ? sh.lg_c[v1] : sh.newc[v1 - 64];
@@ -1067,9 +1072,12 @@ __device__ __forceinline__ void v_check_grab(Scan2Shared<C>& sh, int qb, int off
         const int v0 = t * VPT + 2 * grp;
         const bool h0 = v0 < C::KVER, h1 = v0 + 1 < C::KVER;
         const int v0s = h0 ? v0 : 0, v1 = h1 ? v0 + 1 : v0s;
-        const int vp0 = h0 ? sh.vpos[v0s] : -1, vp1 = h1 ? sh.vpos[v1] : -1;
-        const bool u0 = vp0 >= 0 && act && j >= sh.vfrom[v0s] && j <= sh.vto[v0s] && vp0 != cs;
-        const bool u1 = vp1 >= 0 && act && j >= sh.vfrom[v1] && j <= sh.vto[v1] && vp1 != cs;
+        // the metadata of both versions in one LDS round trip (no short-circuit
+        // branches between dependent reads)
+        const int4 m0 = sh.vmeta[v0s], m1 = sh.vmeta[v1];
+        const int vp0 = h0 ? m0.x : -1, vp1 = h1 ? m1.x : -1;
+        const bool u0 = (vp0 >= 0) & act & (j >= m0.y) & (j <= m0.z) & (vp0 != cs);
+        const bool u1 = (vp1 >= 0) & act & (j >= m1.y) & (j <= m1.z) & (vp1 != cs);
         if (u0 || u1) {
             const float* c0 = v0s < 64 ? sh.lg_c[v0s] : sh.newc[v0s - 64];
             const float* c1 = v1 < 64 ? sh.lg_c[v1] : sh.newc[v1 - 64];
