@@ -58,6 +58,9 @@
 
 namespace gsc {
 
+#ifndef GSC_DFS_CALL_D
+#define GSC_DFS_CALL_D 8  // feature widths whose exact DFS is an out-of-line call (A/B switch)
+#endif
 #ifndef GSC_EPSF8
 #define GSC_EPSF8 0x1p-18f  // A1 bound slack at D = 8 (< 56u of its 64u, see a1_dist_x2)
 #endif
@@ -2226,7 +2229,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                     // NaN leaves carry +inf here: inert, as the query's descent
                     // reaches a real leaf first (NaN-first queries never fail)
                     dfs_parallel_nan<C>(sh, tid, ln, wave, bpos, key);
-                } else if constexpr (D <= 8) {
+                } else if constexpr (D <= GSC_DFS_CALL_D) {
                     dfs_parallel_call<C>(sh, tid, ln, wave, bpos, key);
                 } else {
                     dfs_parallel<C>(sh, tid, ln, wave, bpos, key);
