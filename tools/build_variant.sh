@@ -12,7 +12,7 @@ out=../lib/variants/$name
 mkdir -p $out
 /opt/rocm/bin/hipcc -O2 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function \
   --offload-arch=gfx950 -fno-gpu-rdc -fno-gpu-flush-denormals-to-zero -fno-slp-vectorize -fno-vectorize \
-  -mllvm -amdgpu-sched-strategy=max-ilp "$@" -c -o $out/gsc_scan.o $src
+  -mllvm -amdgpu-sched-strategy=max-ilp -mllvm -amdgpu-atomic-optimizer-strategy=None "$@" -c -o $out/gsc_scan.o $src
 objs=$(ls ../lib/*.o | grep -v gsc_scan.o)
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $out/libsoundchunks_amd.so $objs $out/gsc_scan.o -lpthread
 echo built $out
