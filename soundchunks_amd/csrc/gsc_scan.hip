@@ -1868,6 +1868,18 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         STAMP(14)  // diagnostic split of "prep": loop top (into a2box's slot) vs the update chain
 #endif
         if (wave == 0 && has_p) vp_begin<C>(sh, P_buf, P_off, P_n, vq_a10, ln, lg_pos, lg_tag, vst);
+        // D = 8: the update chain right after its prep, so the V check can start
+        // as soon as a wave is done with A1 (wave 0 reaches the mid-A1 barrier
+        // early).  C5 -cs4 scan -3.2 % (5551 vs 5732 ms at 128 s) and no VGPR
+        // spill left; at D = 16 +0.6 % (3361 vs 3342 ms), so it stays after A1
+        constexpr bool kVpEarly = NWG == 1 && D <= 8;
+        if constexpr (kVpEarly) {
+            if (wave == 0 && has_p) {
+                vp_end<C>(sh, P_buf, P_off, P_n, ln, lg_pos, vst);
+                wave_lds_sync();
+                if (ln == 0) __hip_atomic_store(&sh.vp_ready, it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
         // prefetch the next batch's queries (they land in LDS in part 3).  Issued
         // after vp_begin: a wait for any later vector-memory op (a scratch reload)
         // waits for this HBM load too, and A1 below issues none
@@ -1949,13 +1961,18 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         } else {
             a1_mask(curm);
         }
-        if (wave == 0 && has_p) vp_end<C>(sh, P_buf, P_off, P_n, ln, lg_pos, vst);
+        if constexpr (!kVpEarly) {
+            if (wave == 0 && has_p) vp_end<C>(sh, P_buf, P_off, P_n, ln, lg_pos, vst);
+        }
         if constexpr (NWG == 1) {
             STAMP(7)  // one-CU frames: slot 7 = the rest of A1 (+ vp_end); slot 1 = the V check below
             if (has_p) {  // V check of the pending batch by the waves done with A1 (v_check_grab)
                 if (wave == 0) {
-                    wave_lds_sync();
-                    if (ln == 0) __hip_atomic_store(&sh.vp_ready, it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if constexpr (!kVpEarly) {
+                        wave_lds_sync();
+                        if (ln == 0)
+                            __hip_atomic_store(&sh.vp_ready, it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
                 } else {
                     while (__hip_atomic_load(&sh.vp_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != it + 1)
                         __builtin_amdgcn_s_sleep(1);
