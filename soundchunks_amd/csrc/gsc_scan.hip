@@ -85,7 +85,9 @@ struct ScanCfg {
     static constexpr int KW = LOGK - 6 - LS >= 0 ? LOGK - 6 - LS : 0;   // kd depths resolved at wave level
     static constexpr int KB = D > 16 ? 16 : 32;                         // queries per speculative batch
     static constexpr int KVER = 64 + KB;                                // centroid versions a pending batch sees
-    static constexpr int QD = D < 16 ? 16 : D;                          // query row stride
+    // query row stride: odd x 16 B at D >= 16, so per-lane rows (box bounds, V check,
+    // update chain) read without b128 bank conflicts (C2 scan -1.0 %: 3332 vs 3366 ms)
+    static constexpr int QD = D < 16 ? 16 : D + 4;
     static constexpr int H = D / 2;  // DCT half of the features; [H, D) = cepstrum x 1e-5 (encoder.lpr:1700-1716)
     static constexpr int ROW = D + 4;  // lane-indexed coordinate rows: 16-B multiple, odd x 16 B (no b128 conflicts)
     // A1 bound slack: eps(q) = (|q|^2 + M) * 2^-EPSX (see a1_dist_x2)
