@@ -21,12 +21,13 @@ Scaling: weak by default (each rank adds --seconds of audio to one longer
 file); --strong keeps one --seconds file for any world size.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--seconds S]
-                  [--config c1|c2|c3|c4|c5|c5cs4|br128] [--strong] [--no-cpu-baseline]
+                  [--config c1|c2|c3|c4|c4d|c5|c5cs4|br128] [--strong] [--no-cpu-baseline]
                   [--backend nccl|gloo]
 
 After the timed loop the last step's output is checked frame by frame against
 the oracle's SHA-256 digests of the same workload (tests/golden/
-bench_digests.json; c4: corpus_meta.json): "bit_exact" in the line, and a
+bench_digests.json; c4 / c4d: corpus_meta.json / corpus_default_meta.json):
+"bit_exact" in the line, and a
 mismatch exits with status 3.
 
 --gpus N without a launcher's WORLD_SIZE spawns N worker processes (one per
@@ -58,14 +59,20 @@ CONFIGS = {
     "br128": (["-br128", "-vfr0.5", "-cs8"], 2, 44100, 8, "44.1 kHz stereo, -br128 -vfr0.5 ChunkSize=8"),
     # configs[3]: the reference's lame_test corpus (22 mono 44.1 kHz files) as one batch, default flags
     "c4": (["-cs8", "-cpf4096"], 1, 44100, 8, "lame_test corpus (22 mono 44.1 kHz files), ChunkSize=8 ChunkCount=4096"),
+    # configs[3] at the flags SURVEY.md §8d gives it ("all other flags default"): the encoder
+    # defaults -cs4 -cpf4096 (encoder.lpr:1486-1509; encoder.lps:260 `mstest.wav -v`)
+    "c4d": ([], 1, 44100, 4, "lame_test corpus (22 mono 44.1 kHz files), encoder defaults (ChunkSize=4 ChunkCount=4096)"),
 }
+CORPUS_CONFIGS = ("c4", "c4d")
 CORPUS = ROOT / "tests" / "golden" / "lame_test"
 
 VALU_F32_PEAK_TOPS = 78.6  # non-fused f32 VALU ops/s: half the 157.3 TFLOPS FMA-counted peak
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md (spec)
 PMC_SUMMARY = ROOT / "profiles" / "r04" / "pmc_summary.json"  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
 DIGESTS = ROOT / "tests" / "golden" / "bench_digests.json"  # oracle per-frame .gsc digests (make_bench_digests.py)
-CORPUS_META = ROOT / "tests" / "golden" / "corpus_meta.json"  # oracle .gsc digests of the lame_test files
+# oracle .gsc digests of the lame_test files (tests/golden/make_corpus.py)
+CORPUS_META = {"c4": ROOT / "tests" / "golden" / "corpus_meta.json",
+               "c4d": ROOT / "tests" / "golden" / "corpus_default_meta.json"}
 
 
 def _dist_env():
@@ -109,8 +116,8 @@ def cpu_baseline(cfg: str, argv, rate: int, channels: int, frame_seconds: float,
     (encoder.lpr:1449).  Single thread: `runs` independent 1-thread encodes of
     one full frame side by side on separate cores (ctypes releases the GIL),
     median.  All-core: `threads` threads on `threads` full frames of the same
-    signal and flags (c4: the corpus files in order until `threads` frames),
-    one run."""
+    signal and flags (c4 / c4d: the corpus files in order until `threads`
+    frames), median of `runs` runs."""
     import statistics
     import threading
 
@@ -119,7 +126,7 @@ def cpu_baseline(cfg: str, argv, rate: int, channels: int, frame_seconds: float,
     from soundchunks_amd.synth import synth_wav
 
     oracle_ffi.load()
-    if cfg == "c4":
+    if cfg in CORPUS_CONFIGS:
         wavs = [(CORPUS / n).read_bytes() for n in sorted(os.listdir(CORPUS)) if n.endswith(".wav")]
         nfr = [len(oracle_ffi.frame_bounds(w, argv)[0]) for w in wavs]
         one_wav = wavs[int(max(range(len(wavs)), key=lambda i: len(wavs[i]) / max(1, nfr[i])))]
@@ -173,7 +180,7 @@ def cpu_baseline(cfg: str, argv, rate: int, channels: int, frame_seconds: float,
     nsamp = sum((len(w) - 44) // 2 for w in sample)
     allv = nsamp / wn / 1e6
     _, share, quota = _cpu_share()
-    what = (f"{len(sample)} corpus files ({nsamp / rate:.1f} s)" if cfg == "c4"
+    what = (f"{len(sample)} corpus files ({nsamp / rate:.1f} s)" if cfg in CORPUS_CONFIGS
             else f"{threads} full {frame_seconds:g}-s frames ({frame_seconds * threads:g} s) of the same synthetic "
                  f"{rate} Hz {channels}-ch signal and flags")
     return {"value": round(allv, 6), "unit": "Msamples/s", "cores": threads, "kind": "port",
@@ -285,8 +292,8 @@ def main():
 
     argv, ch, rate, cs, desc = CONFIGS[args.config]
     enc = sc.Encoder(argv)
-    if args.config == "c4":
-        return bench_corpus(args, enc, argv, desc, ws, rank, cdev, dist)
+    if args.config in CORPUS_CONFIGS:
+        return bench_corpus(args, enc, argv, desc, ws, rank, cdev, dist, cs)
     total_seconds = args.seconds if args.strong else args.seconds * ws
     wav = synth_wav(total_seconds, rate, ch)  # the job's input, in host memory on every rank
 
@@ -462,7 +469,7 @@ def base_result(args, ws, dt, value, desc, enc, tm, cs, argv, rate, ch) -> dict:
     }
 
 
-def bench_corpus(args, enc, argv, desc, ws, rank, cdev, dist):
+def bench_corpus(args, enc, argv, desc, ws, rank, cdev, dist, cs):
     """configs[3]: the 22-file lame_test corpus as ONE batch -- every frame of
     every file in one device launch per stage (gsc_encode_many), frames of the
     batch sharded across ranks by chunk count, one .gsc per file on rank 0."""
@@ -503,7 +510,7 @@ def bench_corpus(args, enc, argv, desc, ws, rank, cdev, dist):
         return
     n_samples = sum((len(w) - 44) // 2 for w in wavs)
     value = n_samples * args.steps / dt / 1e6
-    result = base_result(args, ws, dt, value, desc, enc, tm, 8, argv, 44100, 1)
+    result = base_result(args, ws, dt, value, desc, enc, tm, cs, argv, 44100, 1)
     result["config"] = {"workload": f"{desc}, {n_samples / 44100:.1f} s of audio in {len(wavs)} files",
                         "files": len(wavs), "frames": tm["frames"], "argv": argv,
                         "parallelism": f"frame-sharded x{ws}"}
@@ -511,18 +518,19 @@ def bench_corpus(args, enc, argv, desc, ws, rank, cdev, dist):
     result["job_latency_ms"] = None if lat is None else round(lat, 1)
     result["realtime_x"] = round(value / (44100 / 1e6), 2)
     result["outputs_bytes"] = sum(len(o) for o in outs)
-    # every file's .gsc of the last timed step against the oracle's digest (corpus_meta.json)
+    # every file's .gsc of the last timed step against the oracle's digest
     import hashlib
 
-    meta = json.loads(CORPUS_META.read_text())
+    meta_path = CORPUS_META[args.config]
+    meta = json.loads(meta_path.read_text())
     bad = sum(hashlib.sha256(o).hexdigest() != meta["files"][n]["gsc_sha256"] for n, o in zip(names, outs))
     if meta["argv"] != list(argv):
         bad = len(names)
     result["bit_exact"] = bad == 0
-    result["bit_exact_check"] = {"digests": "tests/golden/corpus_meta.json (oracle .gsc per file)",
+    result["bit_exact_check"] = {"digests": f"tests/golden/{meta_path.name} (oracle .gsc per file)",
                                  "files_checked": len(names), "files_differing": bad, "whole_file": True}
     if not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline("c4", argv, 44100, 1, enc.frame_length / 1000.0, args.cpu_threads)
+        result["cpu_baseline"] = cpu_baseline(args.config, argv, 44100, 1, enc.frame_length / 1000.0, args.cpu_threads)
     print(json.dumps(result))
     if dist is not None:
         dist.destroy_process_group()

@@ -184,6 +184,7 @@ typedef struct {
     double post_overlap_ms;      /* KNNFit + prune/sort + packing run while other frames were still scanning */
     int post_groups;             /* frame groups the post-processing pipeline ran */
     double gpu_recon_ms;         /* gsc_encode_wav_recon only: reconstruction + PsyADelta sum */
+    long long knnfit_overflow;   /* queries whose tie set exceeded the 64-NN bucket (ANN replay) */
 } gsc_timing;
 void gsc_last_timing(gsc_timing *t);
 

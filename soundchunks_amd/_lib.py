@@ -57,6 +57,7 @@ class GscTiming(ctypes.Structure):
         ("post_overlap_ms", ctypes.c_double),
         ("post_groups", ctypes.c_int),
         ("gpu_recon_ms", ctypes.c_double),
+        ("knnfit_overflow", ctypes.c_longlong),
     ]
 
 

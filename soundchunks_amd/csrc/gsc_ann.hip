@@ -440,9 +440,20 @@ __global__ __launch_bounds__(kOvBlock) void knnfit_ann_kernel(const Tree* __rest
             if ((double)box >= (double)mk.max_key()) break;  // box * (1 + eps)^2, eps = 0
             int h = nd.x, s = nd.y, n = nd.z;
             for (;;) {  // ANNkd_split::ann_pri_search: push the far child, descend the near one
+                // bounds check (the replay's arrays are poison-filled, gsc_runtime.cpp
+                // DevArena): a node, segment or point index outside its tree's
+                // arrays reports -4 instead of reading another frame's memory
+                if (s < 0 || n < 1 || s + n > t.n || (t.ncap > 0 && (h < 0 || h >= t.ncap))) {
+                    out[job.out] = -4;
+                    return;
+                }
                 if (n == 1) {
                     const float min_dist = mk.max_key();
                     const int pi = t.pidx[s];
+                    if (pi < 0 || pi >= t.n) {
+                        out[job.out] = -4;
+                        return;
+                    }
                     const float* pp = t.pts + (int64_t)pi * t.dd;
                     float dist = 0.0f;
                     int d;
@@ -454,6 +465,10 @@ __global__ __launch_bounds__(kOvBlock) void knnfit_ann_kernel(const Tree* __rest
                     break;
                 }
                 const int half = n >> 1, cdim = t.cd[h];
+                if (cdim < 0 || cdim >= t.dd) {  // an unbuilt node (poison -1)
+                    out[job.out] = -4;
+                    return;
+                }
                 const float cut = fs(q[cdim], t.cv[h]);
                 float bd;
                 int nh, ns, nn, fh, fs_, fn;

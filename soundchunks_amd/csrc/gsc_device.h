@@ -118,6 +118,7 @@ struct AnnTree {
     float* hi;
     float* bnd;        // 2 * dd: bounding rect lo | hi
     float* val;        // n floats of build scratch (the staged cut values)
+    int ncap;          // entries of cd / cv / lo / hi (0: unchecked; the KNNFit overflow replay sets it)
 };
 
 // One KNNFit query whose tie set exceeds ANN's 64-NN bucket: replayed through

@@ -162,22 +162,49 @@ struct DevBuf {
     }
 };
 
-// stream-ordered device buffer (hipMallocAsync / hipFreeAsync on one stream);
-// on the null stream (the synchronous drop-in ABI calls) plain hipMalloc / hipFree
-template <typename T>
-struct StreamBuf {
-    T* p = nullptr;
-    hipStream_t st;
-    explicit StreamBuf(hipStream_t s) : st(s) {}
-    ~StreamBuf() {
-        if (!p) return;
-        if (st) (void)hipFreeAsync(p, st);
-        else (void)hipFree(p);
+// Device scratch of the KNNFit overflow replay: one grow-only hipMalloc
+// block carved into aligned sub-buffers, owned by the caller (the encode's
+// PostCtx, or the synchronous drop-in call) and freed only when the caller is
+// done.  Round 4 ran the replay on stream-ordered pool memory
+// (hipMallocAsync / hipFreeAsync); a second replay in one process faulted on
+// the null stream, and the workaround there (plain hipMalloc) left the pool
+// path in the encoder.  The arena replaces both: no pool, no free while a
+// replay can still be in flight (hipFree of a retired block waits for the
+// device, so retired blocks are kept until the owner is destroyed), and every
+// sub-buffer is poison-filled (0xff bytes: NaN floats, -1 ints) before each
+// replay, so a read of memory the replay did not write cannot hide behind the
+// zero pages a fresh hipMalloc returns -- the GPU tests run the replay twice
+// per process on both streams against the oracle.
+struct DevArena {
+    char* p = nullptr;
+    size_t cap = 0, used = 0;
+    std::vector<char*> retired;
+    ~DevArena() {
+        if (p) (void)hipFree(p);
+        for (char* r : retired) (void)hipFree(r);
     }
-    hipError_t alloc(size_t count) {
-        const size_t bytes = sizeof(T) * std::max<size_t>(count, 1);
-        if (!st) return hipMalloc(reinterpret_cast<void**>(&p), bytes);
-        return hipMallocAsync(reinterpret_cast<void**>(&p), bytes, st);
+    static size_t round_up(size_t b) { return (std::max<size_t>(b, 1) + 255) & ~size_t(255); }
+    // make room for `bytes` (the sum of round_up of every take of one replay)
+    hipError_t reset(size_t bytes) {
+        used = 0;
+        if (bytes <= cap) return hipSuccess;
+        if (p) retired.push_back(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = std::max<size_t>(bytes + bytes / 4, size_t(1) << 20);
+        const double t = now_ms();
+        const hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), want);
+        g_devbuf_ns.fetch_add(int64_t((now_ms() - t) * 1e6));
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    template <typename T>
+    T* take(size_t count) {
+        const size_t b = round_up(sizeof(T) * count);
+        if (used + b > cap) return nullptr;
+        T* r = reinterpret_cast<T*>(p + used);
+        used += b;
+        return r;
     }
 };
 
@@ -436,7 +463,7 @@ int run_reduce_batch(int D, int K, int precision, const std::vector<int>& Ns, co
 // rule for every such query (gsc_ann.hip knnfit_ann_kernel).
 int run_knnfit_overflow(int CS, const std::vector<FitFrame>& fr, const std::vector<int>& ov_frames,
                         const std::vector<float>& eps, const std::vector<float>& cand, const std::vector<float>& q,
-                        std::vector<int>* best, hipStream_t st) {
+                        std::vector<int>* best, hipStream_t st, DevArena* arena) {
     const int nt = int(ov_frames.size());
     const double t_begin = now_ms();
     std::vector<float> pts;
@@ -481,43 +508,57 @@ int run_knnfit_overflow(int CS, const std::vector<FitFrame>& fr, const std::vect
     }
     if (jobs.empty()) return 0;
     if (q.size() > size_t(INT32_MAX)) return fail("KNNFit overflow: query slab exceeds 2^31 floats");
-    // stream-ordered buffers: the replay runs on the caller's stream (the
-    // post-processing stream during the scan) and never syncs the device
-    StreamBuf<float> dPts(st), dCv(st), dLo(st), dHi(st), dBnd(st), dQ(st), dPqk(st), dVal(st);
-    StreamBuf<int> dPidx(st), dCd(st), dOut(st);
-    StreamBuf<AnnTree> dTrees(st);
-    StreamBuf<KnnOvJob> dJobs(st);
-    StreamBuf<int4> dPqn(st);
-    HIP_TRY(dPts.alloc(pts.size()));
-    HIP_TRY(dPidx.alloc(size_t(pts.size() / size_t(CS))));
-    HIP_TRY(dVal.alloc(size_t(pts.size() / size_t(CS))));
-    HIP_TRY(dCd.alloc(size_t(nodes)));
-    HIP_TRY(dCv.alloc(size_t(nodes)));
-    HIP_TRY(dLo.alloc(size_t(nodes)));
-    HIP_TRY(dHi.alloc(size_t(nodes)));
-    HIP_TRY(dBnd.alloc(size_t(2 * CS * nt)));
-    HIP_TRY(dTrees.alloc(size_t(nt)));
-    HIP_TRY(dQ.alloc(q.size()));
-    HIP_TRY(dOut.alloc(best->size()));
-    HIP_TRY(hipMemcpyAsync(dPts.p, pts.data(), sizeof(float) * pts.size(), hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemsetAsync(dCd.p, 0xff, sizeof(int) * size_t(nodes), st));
-    HIP_TRY(hipMemcpyAsync(dQ.p, q.data(), sizeof(float) * q.size(), hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(dOut.p, best->data(), sizeof(int) * best->size(), hipMemcpyHostToDevice, st));
+    // the box queues (<= one push per split node each): bounded launches
+    const int pq_cap = max_n + 2;
+    const size_t per_job = size_t(pq_cap) * (sizeof(float) + sizeof(int4));
+    const int chunk = int(std::max<size_t>(64, std::min<size_t>(jobs.size(), (size_t(2) << 30) / per_job)));
+    // the caller's arena (no allocation on the replay's stream, nothing freed
+    // before the owner is done); every sub-buffer poison-filled below
+    const size_t npts = pts.size() / size_t(CS);
+    const size_t R = DevArena::round_up(sizeof(float) * pts.size()) + 2 * DevArena::round_up(sizeof(float) * npts) +
+                     2 * DevArena::round_up(sizeof(int) * size_t(nodes)) + 2 * DevArena::round_up(sizeof(float) * size_t(nodes)) +
+                     DevArena::round_up(sizeof(int) * npts) + DevArena::round_up(sizeof(float) * size_t(2 * CS * nt)) +
+                     DevArena::round_up(sizeof(AnnTree) * size_t(nt)) + DevArena::round_up(sizeof(float) * q.size()) +
+                     DevArena::round_up(sizeof(int) * best->size()) + DevArena::round_up(sizeof(KnnOvJob) * jobs.size()) +
+                     DevArena::round_up(sizeof(float) * size_t(chunk) * pq_cap) +
+                     DevArena::round_up(sizeof(int4) * size_t(chunk) * pq_cap);
+    HIP_TRY(arena->reset(R));
+    float* dPts = arena->take<float>(pts.size());
+    int* dPidx = arena->take<int>(npts);
+    float* dVal = arena->take<float>(npts);
+    int* dCd = arena->take<int>(size_t(nodes));
+    float* dCv = arena->take<float>(size_t(nodes));
+    float* dLo = arena->take<float>(size_t(nodes));
+    float* dHi = arena->take<float>(size_t(nodes));
+    float* dBnd = arena->take<float>(size_t(2 * CS * nt));
+    AnnTree* dTrees = arena->take<AnnTree>(size_t(nt));
+    float* dQ = arena->take<float>(q.size());
+    int* dOut = arena->take<int>(best->size());
+    KnnOvJob* dJobs = arena->take<KnnOvJob>(jobs.size());
+    float* dPqk = arena->take<float>(size_t(chunk) * pq_cap);
+    int4* dPqn = arena->take<int4>(size_t(chunk) * pq_cap);
+    (void)dVal;
+    if (!dPqn) return fail("KNNFit overflow: replay arena too small");
+    HIP_TRY(hipMemsetAsync(arena->p, 0xff, arena->used, st));  // poison (dCd's -1 marks unbuilt nodes too)
+    HIP_TRY(hipMemcpyAsync(dPts, pts.data(), sizeof(float) * pts.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(dQ, q.data(), sizeof(float) * q.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(dOut, best->data(), sizeof(int) * best->size(), hipMemcpyHostToDevice, st));
     std::vector<AnnTree> trees(static_cast<size_t>(nt));
     for (int t = 0; t < nt; ++t) {
         AnnTree& a = trees[size_t(t)];
-        a.pts = dPts.p + pt_off[t];
+        a.pts = dPts + pt_off[t];
         a.n = 4 * fr[size_t(ov_frames[t])].R;
         a.dd = CS;
-        a.pidx = dPidx.p + pt_off[t] / CS;
-        a.cd = dCd.p + nd_off[t];
-        a.cv = dCv.p + nd_off[t];
-        a.lo = dLo.p + nd_off[t];
-        a.hi = dHi.p + nd_off[t];
-        a.bnd = dBnd.p + size_t(2 * CS) * size_t(t);
-        a.val = dVal.p + pt_off[t] / CS;
+        a.pidx = dPidx + pt_off[t] / CS;
+        a.cd = dCd + nd_off[t];
+        a.cv = dCv + nd_off[t];
+        a.lo = dLo + nd_off[t];
+        a.hi = dHi + nd_off[t];
+        a.bnd = dBnd + size_t(2 * CS) * size_t(t);
+        a.val = dVal + pt_off[t] / CS;
+        a.ncap = caps[t];
     }
-    HIP_TRY(hipMemcpyAsync(dTrees.p, trees.data(), sizeof(AnnTree) * size_t(nt), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(dTrees, trees.data(), sizeof(AnnTree) * size_t(nt), hipMemcpyHostToDevice, st));
     const bool timing = std::getenv("GSC_HOST_TIMING") != nullptr;
     struct EvPair {  // diagnostic events, released on every return path
         hipEvent_t a = nullptr, b = nullptr;
@@ -533,21 +574,14 @@ int run_knnfit_overflow(int CS, const std::vector<FitFrame>& fr, const std::vect
         HIP_TRY(hipEventCreate(&eb1));
         HIP_TRY(hipEventRecord(eb0, st));
     }
-    HIP_TRY(gsc_launch_ann_build_many(dTrees.p, nt, st));
+    HIP_TRY(gsc_launch_ann_build_many(dTrees, nt, st));
     if (timing) HIP_TRY(hipEventRecord(eb1, st));
-    // the box queues (<= one push per split node each): bounded launches
-    const int pq_cap = max_n + 2;
-    const size_t per_job = size_t(pq_cap) * (sizeof(float) + sizeof(int4));
-    const int chunk = int(std::max<size_t>(64, std::min<size_t>(jobs.size(), (size_t(2) << 30) / per_job)));
-    HIP_TRY(dPqk.alloc(size_t(chunk) * pq_cap));
-    HIP_TRY(dPqn.alloc(size_t(chunk) * pq_cap));
-    HIP_TRY(dJobs.alloc(jobs.size()));
-    HIP_TRY(hipMemcpyAsync(dJobs.p, jobs.data(), sizeof(KnnOvJob) * jobs.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(dJobs, jobs.data(), sizeof(KnnOvJob) * jobs.size(), hipMemcpyHostToDevice, st));
     for (size_t j0 = 0; j0 < jobs.size(); j0 += size_t(chunk)) {
         const int nj = int(std::min<size_t>(size_t(chunk), jobs.size() - j0));
-        HIP_TRY(gsc_launch_knnfit_ann(dTrees.p, dJobs.p + j0, nj, dQ.p, dOut.p, dPqk.p, dPqn.p, pq_cap, st));
+        HIP_TRY(gsc_launch_knnfit_ann(dTrees, dJobs + j0, nj, dQ, dOut, dPqk, dPqn, pq_cap, st));
     }
-    HIP_TRY(hipMemcpyAsync(best->data(), dOut.p, sizeof(int) * best->size(), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(best->data(), dOut, sizeof(int) * best->size(), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     if (timing) {
         float bms = 0.0f;
@@ -555,8 +589,11 @@ int run_knnfit_overflow(int CS, const std::vector<FitFrame>& fr, const std::vect
         std::fprintf(stderr, "KNNFit overflow: %d trees (largest %d candidates), %zu queries, %.2f ms (tree builds %.2f ms)\n",
                      nt, max_n, jobs.size(), now_ms() - t_begin, double(bms));
     }
-    for (const KnnOvJob& j : jobs)
-        if ((*best)[size_t(j.out)] < 0) return fail("KNNFit: ANN priority search emulation failed");
+    for (const KnnOvJob& j : jobs) {
+        const int b = (*best)[size_t(j.out)];
+        if (b == -4) return fail("KNNFit overflow: a tree index left its frame's arrays (device bounds check)");
+        if (b < 0) return fail("KNNFit: ANN priority search emulation failed");
+    }
     return 0;
 }
 
@@ -620,7 +657,8 @@ int run_knnfit_batch(int CS, const std::vector<int>& Rs, const std::vector<int>&
             qh.resize(size_t(qo));
             HIP_TRY(hipMemcpy(qh.data(), qdev, sizeof(float) * size_t(qo), hipMemcpyDeviceToHost));
         }
-        if (run_knnfit_overflow(CS, fr, ov_frames, eps, cand, q.empty() ? qh : q, best, nullptr) != 0) return -1;
+        DevArena arena;  // synchronous call: freed on return, after the stream sync
+        if (run_knnfit_overflow(CS, fr, ov_frames, eps, cand, q.empty() ? qh : q, best, nullptr, &arena) != 0) return -1;
         if (knn_ms) *knn_ms += now_ms() - t0;
     }
     return 0;
@@ -677,6 +715,7 @@ struct PostCtx {
     DevBuf<uint32_t> dWords, dCodes;
     DevBuf<FitFrame> dFit;
     DevBuf<PackFrame> dPack;
+    DevArena ov_arena;  // KNNFit overflow replay scratch (kept until the encode is done)
     const float* dQry = nullptr;
     float* hCand = nullptr;
     int *hCnt = nullptr, *hRemap = nullptr;
@@ -684,6 +723,7 @@ struct PostCtx {
     int slot = 0;  // next descriptor slot in dFit / dPack
     double knn_ms = 0;
     int groups = 0;
+    long long ov_queries = 0;  // KNNFit queries replayed through ANN's priority search
     ~PostCtx() {
         if (st) {
             (void)hipStreamSynchronize(st);
@@ -975,7 +1015,8 @@ int Encoder::post_group(std::vector<FrameState>& frames, const std::vector<int>&
             lf.push_back(x);
         }
         if (!chk(hipStreamSynchronize(st), "download")) return -1;
-        if (run_knnfit_overflow(cs, lf, lidx, leps, lcand, lq, &lbest, st) != 0) {
+        c.ov_queries += std::count(lbest.begin(), lbest.end(), -1);
+        if (run_knnfit_overflow(cs, lf, lidx, leps, lcand, lq, &lbest, st, &c.ov_arena) != 0) {
             *err = t_err;
             return -1;
         }
@@ -1345,6 +1386,7 @@ int Encoder::encode_range(int b, int e, std::vector<uint8_t>* out, std::string* 
         tim->gpu_recon_ms = recon_ms;
         tim->post_overlap_ms = overlap_ms;
         tim->post_groups = pc.groups;
+        tim->knnfit_overflow = pc.ov_queries;
         tim->frames = nfr;
         tim->reduce_frames = int(red_idx.size());
         long long pts = 0;

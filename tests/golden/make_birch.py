@@ -74,6 +74,9 @@ if __name__ == "__main__" and sys.argv[1:2] != ["--files"]:
 # frame, then the oracle encodes with them (oracle_ffi.set_py_labels)
 PY_FILES = {
     "mstest_fl500_cpf256_py": ("lame_test/mstest.wav", ["-fl500", "-cpf256", "-py"]),
+    # encoder/encoder.lps:261 `mstest.wav -v -py`: the defaults (-cs4 -cpf4096),
+    # Birch at K = 4096 on N ~ 43,750 rows per frame
+    "mstest_default_py": ("lame_test/mstest.wav", ["-py"]),
     # full-length frames: 4.5 s mono at ChunkSize 4 -> N ~ 44100 chunks per frame
     "tone_lsb45_cs4_cpf256_py": ("tone_lsb45", ["-cs4", "-cpf256", "-py"]),
 }

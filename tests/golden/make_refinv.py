@@ -40,6 +40,16 @@ FILES = {
     "tone26.wav": REF / "my_test" / "tone26.wav",
     "testxn32.wav": REF / "my_test" / "testxn32.wav",
     "testn.wav": REF / "my_test" / "testn.wav",
+    # the rest of the reference's opus_test/ and my_test/ inputs (round 5)
+    "mo_10_32.wav": REF / "opus_test" / "mo_10_32.wav",
+    "mo_62_32.wav": REF / "opus_test" / "mo_62_32.wav",
+    "mo_10_44_new.wav": REF / "opus_test" / "mo_10_44_new.wav",
+    "mo_10_48_new.wav": REF / "opus_test" / "mo_10_48_new.wav",
+    "test2.wav": REF / "my_test" / "test2.wav",
+    "testenv.wav": REF / "my_test" / "testenv.wav",
+    "testn26.wav": REF / "my_test" / "testn26.wav",
+    "testxn.wav": REF / "my_test" / "testxn.wav",
+    "testn44.wav": REF / "my_test" / "testn44.wav",
 }
 # name -> (input, argv); encoder.lps:260-279 item numbers in the comments
 CASES = {
@@ -56,6 +66,15 @@ CASES = {
     "tone26_default": ("tone26.wav", []),
     "testxn32_default": ("testxn32.wav", []),
     "testn_default": ("testn.wav", []),
+    "mo_10_32_default": ("mo_10_32.wav", []),
+    "mo_62_32_default": ("mo_62_32.wav", []),
+    "mo_10_44_new_default": ("mo_10_44_new.wav", []),
+    "mo_10_48_new_default": ("mo_10_48_new.wav", []),
+    "test2_default": ("test2.wav", []),
+    "testenv_default": ("testenv.wav", []),
+    "testn26_default": ("testn26.wav", []),
+    "testxn_default": ("testxn.wav", []),
+    "testn44_default": ("testn44.wav", []),
 }
 
 

@@ -79,6 +79,27 @@ def test_knnfit_bucket_overflow_follows_ann_order(oracle, name):
     assert (tr["knn_best"][quiet] > np.flatnonzero(np.abs(cand).sum(axis=1) == 0)[0]).any()
 
 
+def test_knnfit_overflow_replay_twice_per_stream(oracle):
+    """ADVICE r04 regression: the ANN replay of bucket-overflow queries runs
+    twice in one process on the null stream (the synchronous stage entry
+    point) and twice on the encoder's non-blocking post-processing stream,
+    interleaved.  Its device scratch is poison-filled before every replay
+    (gsc_runtime.cpp DevArena) and the replay kernel bounds-checks every node,
+    segment and point index, so a stale or uninitialised read shows up as a
+    wrong answer or a -4 failure here instead of hiding behind zero pages."""
+    import soundchunks_amd as sc
+
+    name = "quiet_tone_cs8_cpf1024"
+    tr = _trace(oracle, name)
+    make, argv = CASES[name]
+    wav, expected = make(), golden_path(name).read_bytes()
+    for _ in range(2):
+        best = sc.knnfit_assign(tr["knn_cand"][0::4], tr["knn_query"], tr["knn_eps"])
+        np.testing.assert_array_equal(best, tr["knn_best"])
+        assert sc.Encoder(argv).encode(wav) == expected
+        assert sc.Encoder.last_timing()["knnfit_overflow"] > 0  # the encoder's stream did replay
+
+
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_gsc_matches_golden(name):
     import soundchunks_amd as sc
@@ -207,13 +228,18 @@ def test_knnfit_eps_boundary_sweep(oracle):
 
 
 # C4: the reference's lame_test corpus (tests/golden/lame_test, copied from the
-# reference as data) at -cs8 -cpf4096; expected digests from the oracle
-# (tests/golden/make_corpus.py)
-def _corpus():
+# reference as data) at -cs8 -cpf4096 (corpus_meta.json) and at the encoder
+# defaults -cs4 -cpf4096 (corpus_default_meta.json: SURVEY.md §8d's C4 flags,
+# encoder.lpr:1486-1509, and encoder.lps:260 `mstest.wav -v`); expected
+# digests from the oracle (tests/golden/make_corpus.py)
+CORPUS_SETS = {"cs8": "corpus_meta.json", "default": "corpus_default_meta.json"}
+
+
+def _corpus(which="cs8"):
     import json
     from golden.cases import HERE
 
-    return json.loads((HERE / "corpus_meta.json").read_text())
+    return json.loads((HERE / CORPUS_SETS[which]).read_text())
 
 
 @pytest.mark.parametrize("name", sorted(_corpus()["files"]))
@@ -232,17 +258,20 @@ def test_corpus_matches_oracle(name):
     assert hashlib.sha256(got).hexdigest() == want["gsc_sha256"]
 
 
-def test_corpus_as_one_batch_matches_oracle():
+@pytest.mark.parametrize("which", sorted(CORPUS_SETS))
+def test_corpus_as_one_batch_matches_oracle(which):
     """C4 (BASELINE configs[3]): all 22 corpus files in ONE batched encode --
     every frame of every file in one launch per stage (gsc_prepare_many /
-    gsc_encode_prepared_files) -- and each file's .gsc equals the oracle's."""
+    gsc_encode_prepared_files) -- and each file's .gsc equals the oracle's;
+    at -cs8 -cpf4096 and at the encoder defaults (-cs4 -cpf4096, D = 8)."""
     import hashlib
 
     import soundchunks_amd as sc
     from golden.cases import HERE
 
-    meta = _corpus()
+    meta = _corpus(which)
     names = sorted(meta["files"])
+    assert len(names) == 22
     wavs = [(HERE / "lame_test" / n).read_bytes() for n in names]
     outs = sc.encode_many(wavs, meta["argv"])
     tm = sc.Encoder.last_timing()
@@ -287,7 +316,7 @@ def test_birch_labels_match_cluster_py(name):
     assert int((got != z["labels"]).sum()) == 0
 
 
-@pytest.mark.parametrize("name", ["mstest_fl500_cpf256_py", "tone_lsb45_cs4_cpf256_py"])
+@pytest.mark.parametrize("name", ["mstest_fl500_cpf256_py", "tone_lsb45_cs4_cpf256_py", "mstest_default_py"])
 def test_python_reduce_file_matches_golden(name):
     import hashlib
     import json

@@ -153,9 +153,11 @@ def test_yakmo_seed_means_properties():
                                     lab.ctypes.data_as(ctypes.POINTER(ctypes.c_int))) == -1
 
 
+@pytest.mark.parametrize("meta_file", ["corpus_meta.json", "corpus_default_meta.json"])
 @pytest.mark.parametrize("name", ["60.wav", "hihat.wav", "mstest.wav"])
-def test_oracle_reproduces_corpus_digest(name):
-    """The committed C4 digests (tests/golden/corpus_meta.json) are what the
+def test_oracle_reproduces_corpus_digest(name, meta_file):
+    """The committed C4 digests (tests/golden/corpus_meta.json at -cs8
+    -cpf4096, corpus_default_meta.json at the encoder defaults) are what the
     oracle computes now (the three smallest corpus files, to stay fast)."""
     import hashlib
     import json
@@ -163,7 +165,7 @@ def test_oracle_reproduces_corpus_digest(name):
     import oracle_ffi
     from golden.cases import HERE
 
-    meta = json.loads((HERE / "corpus_meta.json").read_text())
+    meta = json.loads((HERE / meta_file).read_text())
     wav = (HERE / "lame_test" / name).read_bytes()
     gsc = oracle_ffi.encode(wav, meta["argv"], threads=8)
     assert hashlib.sha256(gsc).hexdigest() == meta["files"][name]["gsc_sha256"]
