@@ -72,7 +72,7 @@ typedef struct {
     double low_cut;       /* -lc, default 0 (band-pass filtering unsupported) */
     double high_cut;      /* -hc, default 24000 */
     int chunk_bit_depth;  /* -cbd, default 8 (8 or 12) */
-    int chunk_size;       /* -cs, default 4 (4, 8 or 16) */
+    int chunk_size;       /* -cs, default 4 (1 .. 16) */
     int chunks_per_frame; /* -cpf, default 4096, clamped [256, 4096] */
     int reduce_bass_band; /* !-pbb, default 1 */
     double vfr;           /* -vfr, default 1.0 */
@@ -117,8 +117,10 @@ gsc_prepared *gsc_prepare(const uint8_t *wav, size_t wav_len, const gsc_options 
 int gsc_prepared_frame_count(const gsc_prepared *p);
 int gsc_prepared_frame_chunks(const gsc_prepared *p, int *chunks);
 int gsc_encode_prepared(gsc_prepared *p, int frame_begin, int frame_end, uint8_t **out, size_t *out_len);
-/* gsc_encode_prepared, plus each frame's share of the returned bytes
- * (frame_bytes[i - frame_begin], frame_end - frame_begin entries): a .gsc is
+/* gsc_encode_prepared, plus each frame's share of the returned bytes.  The
+ * range is clamped first (as in gsc_encode_prepared): b = max(frame_begin, 0),
+ * e = frame_end < 0 ? frame_count : min(frame_end, frame_count); frame_bytes
+ * receives max(e - b, 0) entries, frame_bytes[i - b] for frame i.  A .gsc is
  * the concatenation of its frames' TFrame.SaveStream bytes
  * (encoder.lpr:980-1107, 1181-1215), so the caller can split it per frame
  * (bench.py's per-frame bit-exactness digests).  Every prepared entry point

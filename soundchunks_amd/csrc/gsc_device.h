@@ -48,7 +48,6 @@ struct ReduceFrame {
     int32_t restarts;     // out: batched-pipeline restarts (diagnostic)
     int32_t loop_iters;   // out: batched-pipeline iterations (diagnostic); -1 = guard tripped
     int32_t tree_exact;   // out: passes whose kd-tree needed the sequential build (median ties)
-    int32_t xseq;         // two-CU frames: tag of the last hand-off between the two CUs
     int32_t dcol;         // colCount = 2*ChunkSize (the residual's divisor, encoder.lpr:743); 0 = the slab width
     uint64_t t_done;      // out: s_memrealtime (100 MHz) when the batched kernel finished the frame
     // optional (batched kernel): when the frame is done, its final clusters are

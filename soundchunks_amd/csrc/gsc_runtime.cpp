@@ -35,8 +35,7 @@ extern "C" hipError_t gsc_launch_scan_pass(int D, gsc::ReduceFrame* frames, int 
                                            int only_flagged, hipStream_t st);
 extern "C" hipError_t gsc_launch_scan_batch(int D, int logk, gsc::ReduceFrame* frames, int nframes, const float* X,
                                             float* C, int* is, const float* rate_tab, double tol, int max_passes,
-                                            uint64_t* xbuf, int opts, float* tails, hipStream_t st);
-extern "C" size_t gsc_scan_xbuf_granules_per_frame(void);
+                                            int opts, float* tails, hipStream_t st);
 extern "C" size_t gsc_scan_tail_floats_per_frame(int D, int logk);
 extern "C" hipError_t gsc_launch_atten(int cs, gsc::DspFrame* frames, int nframes, const double* samp, int64_t span,
                                        int ch, int obd, hipStream_t st);
@@ -240,10 +239,6 @@ bool batched_scan_shape(int D, int K) {
     return (D == 8 || D == 16 || D == 32) && K >= 2 && K <= 4096;
 }
 
-// no batched shape runs a frame on two CUs any more (the kernel keeps the
-// hand-off protocol for a future wide shape; xbuf stays unallocated)
-bool two_cu_frames(int, int) { return false; }
-
 // split-layout tail array offset of frame i (frames' slots of the largest size)
 int64_t tail_offset(int i) { return int64_t(i) * 4096 * 16; }
 
@@ -258,13 +253,6 @@ hipError_t launch_scan_passes(int D, ReduceFrame* dfr, int nf, int K, const floa
                               const float* rate, int precision) {
     const double tol = scan_tolerance(precision);
     const bool batched = batched_scan_shape(D, K);
-    DevBuf<uint64_t> xbuf;
-    if (batched && two_cu_frames(D, K)) {
-        const size_t n = gsc_scan_xbuf_granules_per_frame() * size_t(nf);
-        hipError_t e = xbuf.alloc(n);
-        if (e == hipSuccess) e = hipMemset(xbuf.p, 0, sizeof(uint64_t) * n);
-        if (e != hipSuccess) return e;
-    }
     int logk = 0;
     while ((1 << logk) < padded_k(K)) ++logk;
     DevBuf<float> tails;  // split layout: every frame's tail features (ReduceFrame::t_off)
@@ -285,7 +273,7 @@ hipError_t launch_scan_passes(int D, ReduceFrame* dfr, int nf, int K, const floa
             // bit 1 (GSC_SCAN_NO_PRUNE, experiment): no per-wave A1 pruning
             const int opts = (std::getenv("GSC_SCAN_FULL_A1") ? 1 : 0) | (std::getenv("GSC_SCAN_NO_PRUNE") ? 2 : 0);
             hipError_t e =
-                gsc_launch_scan_batch(D, logk, dfr, nf, X, C, is, rate, tol, max_passes, xbuf.p, opts, tails.p, nullptr);
+                gsc_launch_scan_batch(D, logk, dfr, nf, X, C, is, rate, tol, max_passes, opts, tails.p, nullptr);
             if (e != hipSuccess) return e;
             // the generic kernel runs only when the batched one handed a frame
             // over (an empty launch of it still costs ~30 ms: 256 large-LDS

@@ -12,17 +12,16 @@
 // Layout: the K = 2^LOGK centroids live in VGPRs, SL consecutive kd-leaf
 // positions per lane, so every kd subtree is an aligned block of (virtual)
 // waves, lanes and slots: leaf position p = (vwave*64 + lane)*SL + slot.
-//   D <= 16 (ChunkSize 4, 8): one CU per frame, SL = 8 (K = 4096: 8 waves x
+//   D <= 16 (ChunkSize <= 8): one CU per frame, SL = 8 (K = 4096: 8 waves x
 //            64 lanes x 8 leaves x D floats).
-//   D = 32 (ChunkSize 16): 4096 x 32 floats are 512 KB, the whole register
-//            file of a CU, so a frame runs on TWO CUs (NWG = 2), each holding
-//            half of the leaves (the kd root's two subtrees), SL = 4, as one
-//            virtual workgroup of 16 waves.  Both workgroups run the same
-//            pipeline on the same LDS state; what only one of them can compute
-//            (A1 records of its waves, coordinates of its leaves, exact
-//            distances of its leaves) is handed over through HBM as tagged
-//            8-byte granules (xchg below).  K <= 2048 at D = 32 fits one CU
-//            with SL = 4.
+//   D = 32 (ChunkSize 9 .. 16): 4096 x 32 floats are 512 KB, the whole register
+//            file of a CU, so K = 4096 runs the split layout on one CU: the DCT
+//            half (DR = 16 features) in VGPRs, the cepstrum half in a per-frame
+//            tail array in HBM that only the lane owning a leaf reads and writes.
+//            K <= 2048 at D = 32 keeps every feature in VGPRs.
+// (Two CUs per frame -- each holding half the leaves, A1 records and
+// coordinates exchanged through L2 -- was measured against one CU per frame on
+// launches with fewer frames than CUs and removed: 1.4-1.9x slower)
 //
 // Pipeline, per iteration (batches of KB queries; "current" = the batch
 // whose distances are computed now, "pending" = the previous batch, whose
@@ -66,9 +65,9 @@ namespace gsc {
 #endif
 
 // Shape of one KNNScanReduce pipeline instance.
-template <int D_, int LOGK_, int SL_, int NWG_, int DR_ = D_>
+template <int D_, int LOGK_, int SL_, int DR_ = D_>
 struct ScanCfg {
-    static constexpr int D = D_, LOGK = LOGK_, SL = SL_, NWG = NWG_;
+    static constexpr int D = D_, LOGK = LOGK_, SL = SL_;
     // features held in VGPRs; the other TL (split layout: the cepstrum half)
     // live in a per-frame, position-indexed HBM array that only the lane owning
     // the position reads and writes
@@ -77,10 +76,9 @@ struct ScanCfg {
     static constexpr int K = 1 << LOGK;
     static constexpr int LS = SL == 8 ? 3 : (SL == 4 ? 2 : (SL == 2 ? 1 : 0));  // log2 slots per lane
     static constexpr int LPW = 64 * SL;                                 // leaves per wave
-    static constexpr int KG = K / NWG;                                  // leaves per workgroup
-    static constexpr bool FULL = KG >= LPW;                             // every lane holds SL leaves
-    static constexpr int NWL = FULL ? KG / LPW : 1;                     // waves per workgroup
-    static constexpr int NWV = NWL * NWG;                               // virtual waves
+    static constexpr bool FULL = K >= LPW;                              // every lane holds SL leaves
+    static constexpr int NWL = FULL ? K / LPW : 1;                      // waves per workgroup
+    static constexpr int NWV = NWL;                                     // waves holding leaves
     static constexpr int NT = 64 * NWL;                                 // threads per workgroup
     static constexpr int KW = LOGK - 6 - LS >= 0 ? LOGK - 6 - LS : 0;   // kd depths resolved at wave level
     static constexpr int KB = D > 16 ? 16 : 32;                         // queries per speculative batch
@@ -94,8 +92,7 @@ struct ScanCfg {
     static constexpr float EPSF = D > 16 ? 0x1p-16f : (D > 8 ? 0x1p-17f : GSC_EPSF8);
     static_assert(NWV <= 16, "A2 evaluates up to 16 wave records per query (one per lane of a 16-lane group)");
     static_assert(KB <= 32 && 64 % KB == 0, "batch size");
-    static_assert(NWG == 1 || (FULL && NWL == 8), "two-CU frames: 8 full waves per workgroup");
-    static_assert(!SPLIT || (NWG == 1 && DR == H), "split layout: one CU, the DCT half in registers");
+    static_assert(!SPLIT || DR == H, "split layout: the DCT half in registers");
 };
 
 // float minimum on f32 bit patterns (A1 values may be negative: the batch
@@ -230,10 +227,6 @@ struct Scan2Shared {
     uint32_t wkey[2][C::NWL];  // parallel exact DFS: per-wave next-improvement keys
     alignas(16) float a2s[C::NWL][C::D > 16 ? 2 : 1][64];  // A2 scratch per wave: box terms by dimension
     alignas(16) float a2i[C::NWL][64];                     // box' increments by depth
-    // two-CU frames: coordinates of the partner's winner per query column
-    // (this workgroup's own winner writes straight into the QRec's o[])
-    alignas(16) float lw_p[C::NWG > 1 ? C::KB + 1 : 1][C::D];
-    int xnan;              // two-CU frames: partner's NaN flag of the pass
 };
 
 #ifdef GSC_STAMPS
@@ -324,55 +317,6 @@ __device__ __forceinline__ float seqdist(const float* __restrict__ a, const floa
         s = fadd(s, fmul(t, t));
     }
     return s;
-}
-
-// ---------------------------------------------------------------------------
-// Two-CU frames: hand-offs between the two workgroups of a frame through HBM.
-// A granule is one naturally aligned 8-byte {word, tag} written by one agent-
-// scope store (write-through, single-copy atomic) and read by agent-scope
-// loads until its tag is the exchange's; tags grow by one per exchange and
-// the slots alternate by tag parity, so a slot is rewritten only after the
-// partner has read it (MI355X_MICROARCH.md, hand-off price list:
-// handoff-1to1).  Both workgroups call every exchange in the same order.
-// ---------------------------------------------------------------------------
-constexpr int kXCap = 2048;  // granules per slot (the DFS hands over 2048 distances)
-
-struct XPort {
-    uint64_t* mine;          // this workgroup's two slots [2][kXCap]
-    const uint64_t* theirs;  // the partner's
-    uint32_t seq;            // tag of the last exchange (uniform)
-};
-
-__device__ __forceinline__ void xput(const XPort& x, int i, uint32_t w) {
-    const uint64_t g = ((uint64_t)x.seq << 32) | w;
-    __hip_atomic_store(x.mine + (size_t)(x.seq & 1u) * kXCap + i, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t xget(const XPort& x, int i) {
-    const uint64_t* p = x.theirs + (size_t)(x.seq & 1u) * kXCap + i;
-    for (;;) {
-        const uint64_t g = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((uint32_t)(g >> 32) == x.seq) return (uint32_t)g;
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
-
-// barrier between the two workgroups of a frame that also publishes their
-// plain stores (C rows, counts) to each other: every wave drains its stores,
-// one lane releases at agent scope, swaps a granule with the partner and
-// acquires (MI355X_MICROARCH.md: valid producer / consumer forms)
-__device__ __forceinline__ void pair_barrier(XPort& x, int tid) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    ++x.seq;
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        xput(x, 0, 1u);
-        (void)xget(x, 0);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
 }
 
 // ---------------------------------------------------------------------------
@@ -1376,7 +1320,7 @@ __device__ __forceinline__ void refresh(Scan2Shared<C>& sh, float (&creg)[C::SL]
             if constexpr (PAIR) r1[d] = sh.lg_c[e1][d];
         }
         const float nv0 = sh.lg_c[e0][C::ROW - 1], nv1 = sh.lg_c[e1][C::ROW - 1];  // |c|^2, written with the entry
-        if (C::NWG == 1 && lane < D) {  // the pruning box covers the new positions
+        if (lane < D) {  // the pruning box covers the new positions
             const float v0 = sh.lg_c[e0][lane], v1 = sh.lg_c[e1][lane];
             blo = fminf(blo, fminf(v0, v1));
             bhi = fmaxf(bhi, fmaxf(v0, v1));
@@ -1388,7 +1332,7 @@ __device__ __forceinline__ void refresh(Scan2Shared<C>& sh, float (&creg)[C::SL]
             if (two) apply(e1, p1, r1, nv1);
         }
     }
-    if (C::NWG == 1 && lane < D) {
+    if (lane < D) {
         sh.wlo[vwave][lane] = fminf(sh.wlo[vwave][lane], blo);
         sh.whi[vwave][lane] = fmaxf(sh.whi[vwave][lane], bhi);
     }
@@ -1397,11 +1341,10 @@ __device__ __forceinline__ void refresh(Scan2Shared<C>& sh, float (&creg)[C::SL]
 
 // c*'s snapshot coordinates for the queries in qmask (columns col0 + j),
 // written by the lane that owns c* (the first wave / lane / slot at the
-// minimum of the A1 records, as in A2) -- over this workgroup's waves only --
-// into recs[j].o
+// minimum of the A1 records, as in A2) into recs[j].o
 template <class C>
 __device__ __forceinline__ void write_cstar(Scan2Shared<C>& sh, const float (&creg)[C::SL][C::DR], QRecT<C::D>* recs,
-                                            uint64_t qmask, int col0, int wave, int lane, int wg,
+                                            uint64_t qmask, int col0, int wave, int lane,
                                             const float* __restrict__ trow = nullptr) {
     constexpr int SL = C::SL, D = C::D, NWL = C::NWL;
     // lane = query: the winning wave (first at the minimum) and, for this
@@ -1416,7 +1359,7 @@ __device__ __forceinline__ void write_cstar(Scan2Shared<C>& sh, const float (&cr
         int W = 0;
 #pragma unroll
         for (int w = 0; w < NWL; ++w) {
-            const float m = __uint_as_float(sh.wrec[wg * NWL + w][col0 + jq].minbits);
+            const float m = __uint_as_float(sh.wrec[w][col0 + jq].minbits);
             if (m < gm) {
                 gm = m;
                 W = w;
@@ -1424,7 +1367,7 @@ __device__ __forceinline__ void write_cstar(Scan2Shared<C>& sh, const float (&cr
         }
         won = __ballot(act && W == wave);
         if (act && W == wave) {
-            const WaveRecT<SL>& r = sh.wrec[wg * NWL + wave][col0 + jq];
+            const WaveRecT<SL>& r = sh.wrec[wave][col0 + jq];
             bool tie2;
             const int slot = rec_slot<SL>(r, &tie2);
             ol = ((r.lanebits & 255) << 8) | slot;
@@ -1442,140 +1385,34 @@ __device__ __forceinline__ void write_cstar(Scan2Shared<C>& sh, const float (&cr
 #pragma unroll
                 for (int d = 0; d < C::DR; ++d) dst[d] = creg[s][d];
                 if constexpr (C::SPLIT) {
-                    const float* tr = trow + (int64_t)(((wg * NWL + wave) * 64 + owner) * SL + s) * C::TL;
+                    const float* tr = trow + (int64_t)((wave * 64 + owner) * SL + s) * C::TL;
                     for (int d = C::DR; d < D; ++d) dst[d] = tr[d - C::DR];
                 }
             }
     }
 }
 
-// ---- two-CU frames: the exchanges ------------------------------------------
-// this workgroup's winner wave of a column (first at the minimum, as write_cstar)
-template <class C>
-__device__ __forceinline__ int local_winner(const Scan2Shared<C>& sh, int col, int base) {
-    float gm = __builtin_inff();
-    int W = 0;
-#pragma unroll
-    for (int w = 0; w < C::NWL; ++w) {
-        const float m = __uint_as_float(sh.wrec[base + w][col].minbits);
-        if (m < gm) {
-            gm = m;
-            W = w;
-        }
-    }
-    return W;
-}
-
-// A1 records: per query column, the 8 wave minima of this workgroup, its
-// winning wave's whole record and that winner's coordinates; then the 8 wave
-// norm bounds.  The partner's values land in the partner's virtual rows.
-template <class C>
-__device__ __forceinline__ void xchg_records(Scan2Shared<C>& sh, XPort& x, int nq, const int* cols, int col0,
-                                             const QRecT<C::D>* recs, int tid, int wg) {
-    constexpr int D = C::D, NWL = C::NWL, RW = (int)(sizeof(WaveRecT<C::SL>) / 4);
-    constexpr int PQ = NWL + 1 + RW + D;  // words per query
-    const int nw = nq * PQ + NWL;
-    ++x.seq;
-    const int mine0 = wg * NWL, their0 = (1 - wg) * NWL;
-    for (int i = tid; i < nw; i += C::NT) {
-        uint32_t w;
-        if (i < nq * PQ) {
-            const int jq = i / PQ, f = i - jq * PQ;
-            const int col = cols ? col0 + cols[jq] : col0 + jq;
-            if (f < NWL) {
-                w = sh.wrec[mine0 + f][col].minbits;
-            } else if (f == NWL) {
-                w = (uint32_t)local_winner<C>(sh, col, mine0);
-            } else if (f < NWL + 1 + RW) {
-                const int W = local_winner<C>(sh, col, mine0);
-                w = reinterpret_cast<const uint32_t*>(&sh.wrec[mine0 + W][col])[f - NWL - 1];
-            } else {
-                w = __float_as_uint(recs[col - col0].o[f - NWL - 1 - RW]);
-            }
-        } else {
-            w = __float_as_uint(sh.cnmax[mine0 + (i - nq * PQ)]);
-        }
-        xput(x, i, w);
-    }
-    for (int i = tid; i < nw; i += C::NT) {
-        if (i < nq * PQ) {
-            const int jq = i / PQ, f = i - jq * PQ;
-            const int col = cols ? col0 + cols[jq] : col0 + jq;
-            if (f < NWL) {
-                sh.wrec[their0 + f][col].minbits = xget(x, i);
-            } else if (f == NWL) {
-                (void)xget(x, i);
-            } else if (f < NWL + 1 + RW) {
-                const int W = (int)xget(x, jq * PQ + NWL);
-                const uint32_t v = xget(x, i);
-                if (f - NWL - 1 != 0)  // the minbits word is written by the f < NWL branch
-                    reinterpret_cast<uint32_t*>(&sh.wrec[their0 + W][col])[f - NWL - 1] = v;
-            } else {
-                sh.lw_p[col][f - NWL - 1 - RW] = __uint_as_float(xget(x, i));
-            }
-        } else {
-            sh.cnmax[their0 + (i - nq * PQ)] = __uint_as_float(xget(x, i));
-        }
-    }
-}
-
-// after xchg_records: the partner's winner coordinates into o[] of the listed
-// columns where the partner holds the global winner (the lower virtual waves
-// win ties: workgroup 0)
-template <class C>
-__device__ __forceinline__ void fill_winner_coords(Scan2Shared<C>& sh, QRecT<C::D>* recs, int nq, const int* cols,
-                                                   int col0, int tid, int wg) {
-    constexpr int D = C::D, NWL = C::NWL;
-    for (int i = tid; i < nq * D; i += C::NT) {
-        const int jq = i / D, d = i - jq * D;
-        const int j = cols ? cols[jq] : jq;
-        float m0 = __builtin_inff(), m1 = __builtin_inff();
-#pragma unroll
-        for (int w = 0; w < NWL; ++w) {
-            m0 = fminf(m0, __uint_as_float(sh.wrec[w][col0 + j].minbits));
-            m1 = fminf(m1, __uint_as_float(sh.wrec[NWL + w][col0 + j].minbits));
-        }
-        const int gw = m1 < m0 ? 1 : 0;
-        if (gw != wg) recs[j].o[d] = sh.lw_p[col0 + j][d];
-    }
-}
-
 // ---------------------------------------------------------------------------
-// The kernel.  NWG = 1: one workgroup per frame (blockIdx.x = frame).
-// NWG = 2: a cooperative grid of frame pairs; workgroups 2p / 2p + 1 (by
-// default; b and b + 8 when the grid is a multiple of 16, so a pair shares
-// an XCD's L2) run frames p, p + npairs, ...
+// The kernel: one workgroup per frame (blockIdx.x = frame).
 // ---------------------------------------------------------------------------
 template <class C>
 __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restrict__ frames, int nframes,
                                                            const float* __restrict__ Xall, float* __restrict__ Call,
                                                            int* __restrict__ i_scratch,
                                                            const float* __restrict__ rate_tab, double tol,
-                                                           int max_passes, uint64_t* __restrict__ xbuf, int opts,
+                                                           int max_passes, int opts,
                                                            float* __restrict__ Tall) {
-    constexpr int D = C::D, K = C::K, SL = C::SL, LS = C::LS, NWL = C::NWL, KB = C::KB, NWG = C::NWG;
+    constexpr int D = C::D, K = C::K, SL = C::SL, LS = C::LS, NWL = C::NWL, KB = C::KB;
     constexpr int kErrWave = NWL > 1 ? 1 : 0;  // residual + cluster ids (wave 0 keeps the log)
-    constexpr bool PRUNE = NWG == 1;           // A1 pruning by wave boxes (one-CU frames)
+    constexpr bool PRUNE = true;               // A1 pruning by wave boxes
     const bool no_half = (opts & 1) != 0;      // diagnostic: full-dimension A1 bounds in every pass
     const bool no_prune = (opts & 2) != 0;     // experiment: every wave evaluates every query (no mid-A1 barrier)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Scan2Shared<C>& sh = *reinterpret_cast<Scan2Shared<C>*>(smem);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int nthreads = C::NT;
-    int wg = 0, fi0 = blockIdx.x, fstep = nframes;
-    if constexpr (NWG == 2) {
-        const int nb = gridDim.x, b = blockIdx.x;
-        if (nb % 16 == 0) {
-            wg = (b >> 3) & 1;
-            fi0 = (b >> 4) * 8 + (b & 7);
-        } else {
-            wg = b & 1;
-            fi0 = b >> 1;
-        }
-        fstep = nb / 2;
-    }
-    const int vwave = wg * NWL + wave;  // this wave's virtual index
-    const bool wg0 = wg == 0;
+    const int vwave = wave;
+    const int fi0 = blockIdx.x, fstep = nframes;
     for (int fi = fi0; fi < nframes; fi += fstep) {
     ReduceFrame* frp = frames + fi;
     if (uniform_int(frp->done) || uniform_int(frp->generic)) continue;
@@ -1587,7 +1424,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     // ChunksPerFrame that is not a power of two (the -br cost loop,
     // encoder.lpr:1337-1351): ANN's tree over the Kr centroids, embedded in the
     // K = 2^LOGK leaf layout with padding leaves that are never visited (pad_tree)
-    const int Kr = NWG == 1 ? uniform_int(frp->K) : K;
+    const int Kr = uniform_int(frp->K);
     const bool padded = Kr != K;
     const float* __restrict__ X = Xall + uniform_i64(frp->x_off);
     float* C_ = Call + uniform_i64(frp->c_off);
@@ -1596,12 +1433,6 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     int* cnta = i_scratch + uniform_i64(frp->ka_off);     // cnts[Odd(iter)] by kd-leaf position
     // split layout: the tail features of kd-leaf position p at trow + p * TL
     float* trow = C::SPLIT ? Tall + uniform_i64(frp->t_off) : nullptr;
-    XPort xp{nullptr, nullptr, 0};
-    if constexpr (NWG == 2) {
-        xp.mine = xbuf + ((size_t)fi * 2 + wg) * 2 * kXCap;
-        xp.theirs = xbuf + ((size_t)fi * 2 + (1 - wg)) * 2 * kXCap;
-        xp.seq = (uint32_t)uniform_int(frp->xseq);
-    }
     double prev_err = uniform_int(frp->iters) == 0 ? 3.4028234663852886e+38 : frp->err;  // err := MaxSingle
     if constexpr (PRUNE) {  // box of the frame's data in the tail features (half-dimension A1 bounds)
         constexpr int NT_ = D - C::H;
@@ -1631,12 +1462,9 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
 #ifdef GSC_STAMPS
     const uint64_t t_kernel0 = stamp();
 #endif
-    if (pass == 0 && wg0)
+    if (pass == 0)
         for (int k = tid; k < Kr; k += nthreads) prev_cnt[k] = 1;  // CCntStart (encoder.lpr:717-721)
     if (tid == 0) sh.any_nan = 0;
-    if constexpr (NWG == 2) {
-        if (pass == 0) pair_barrier(xp, tid);  // workgroup 1 reads prev_cnt below: workgroup 0 wrote it
-    }
     // NaN rows (yakmo's 0/0 means of seeds that won no point) stay NaN in every
     // pass and finite rows stay finite (c + (x - c) * rate): their leaves carry
     // +inf distances here (inert in ANN's DFS once a real leaf was reached) and
@@ -1666,7 +1494,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         build_tree<D>(sh.t, sh.dist, C_, K);  // one or two leaves per thread: the sequential build
     } else if (!build_tree_fast<D, C::LOGK, nthreads>(sh.t, sh.dist, sh.dfs_inc, C_, &sh.slow_pos)) {
         build_tree<D>(sh.t, sh.dist, C_, K);  // median ties: quickselect's exact order
-        if (tid == 0 && wg0) frp->tree_exact += 1;
+        if (tid == 0) frp->tree_exact += 1;
     }
 
     float creg[SL][C::DR];
@@ -1748,11 +1576,11 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             }
         }
     }
-    // rates of every position (both workgroups of a two-CU frame commit any c*)
+    // rates of every position
     for (int p = tid; p < K; p += nthreads) {
         const int id = sh.t.pidx[p];
         sh.rate[p] = id != 0xFFFF ? rate_tab[prev_cnt[id]] : 0.0f;  // Single(1/sqrt(cnts[not Odd(iter)]))
-        if (wg0) cnta[p] = 1;
+        cnta[p] = 1;
     }
     if (nan_here) sh.any_nan = 1;
     float cnmax;
@@ -1782,16 +1610,6 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         sh.qm[0][k / D][k % D] = -2.0f * x;
     }
     __syncthreads();
-    if constexpr (NWG == 2) {  // agree on NaN and share the wave norm bounds
-        ++xp.seq;
-        if (tid < NWL) xput(xp, tid, __float_as_uint(sh.cnmax[wg * NWL + tid]));
-        if (tid == NWL) xput(xp, NWL, (uint32_t)sh.any_nan);
-        if (tid < NWL) sh.cnmax[(1 - wg) * NWL + tid] = __uint_as_float(xget(xp, tid));
-        if (tid == NWL) sh.xnan = (int)xget(xp, NWL);
-        __syncthreads();
-        if (tid == 0 && sh.xnan) sh.any_nan = 1;
-        __syncthreads();
-    }
     // half-dimension A1 for this pass?  TW over the box of the frame's data
     // and the pass's centroids (tail features), with an ulp-scale slack per
     // feature for the rounding of the online moves
@@ -1826,10 +1644,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         // NaN centroids (yakmo 0/0 means) make ANN's early exits order dependent;
         // the split layout has no full-dimension bound (a tail too wide for eps):
         // this pass runs in the generic kernel (gsc_kernels.hip)
-        if (tid == 0 && wg0) {
-            frp->generic = 1;
-            frp->xseq = (int)xp.seq;
-        }
+        if (tid == 0) frp->generic = 1;
         break;
     }
     if (half) {  // the A1 bounds cover the first H features: H-norms for the bound and for eps's M
@@ -1845,7 +1660,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     int lg_pos = -1, lg_tag = 0;
     double err = 0.0;
     int slow_total = 0, restarts = 0;
-    bool guard = false;  // the progress guard tripped (identical in both workgroups)
+    bool guard = false;  // the progress guard tripped
 #ifdef GSC_STAMPS
     uint64_t acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t acn[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // home, pruned, evaluated, iterations, fixups, pending
@@ -1874,7 +1689,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         // as soon as a wave is done with A1 (wave 0 reaches the mid-A1 barrier
         // early).  C5 -cs4 scan -3.2 % (5551 vs 5732 ms at 128 s) and no VGPR
         // spill left; at D = 16 +0.6 % (3361 vs 3342 ms), so it stays after A1
-        constexpr bool kVpEarly = NWG == 1 && D <= 8;
+        constexpr bool kVpEarly = D <= 8;
         if constexpr (kVpEarly) {
             if (wave == 0 && has_p) {
                 vp_end<C>(sh, P_buf, P_off, P_n, ln, lg_pos, vst);
@@ -1966,8 +1781,8 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         if constexpr (!kVpEarly) {
             if (wave == 0 && has_p) vp_end<C>(sh, P_buf, P_off, P_n, ln, lg_pos, vst);
         }
-        if constexpr (NWG == 1) {
-            STAMP(7)  // one-CU frames: slot 7 = the rest of A1 (+ vp_end); slot 1 = the V check below
+        {
+            STAMP(7)  // slot 7 = the rest of A1 (+ vp_end); slot 1 = the V check below
             if (has_p) {  // V check of the pending batch by the waves done with A1 (v_check_grab)
                 if (wave == 0) {
                     if constexpr (!kVpEarly) {
@@ -1989,25 +1804,11 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         STAMP(1)
         lds_barrier();
         STAMP(6)
-        if constexpr (NWG == 2) {
-            if (cur_n > 0) {
-                write_cstar<C>(sh, creg, sh.qrec[cur_buf], (1ull << cur_n) - 1ull, 0, wave, ln, wg);
-                lds_barrier();
-                xchg_records<C>(sh, xp, cur_n, nullptr, 0, sh.qrec[cur_buf], tid, wg);
-                lds_barrier();
-                fill_winner_coords<C>(sh, sh.qrec[cur_buf], cur_n, nullptr, 0, tid, wg);
-            }
-        }
         // ---- part 2: check the pending batch; certificates of the current batch
         ln = opaque_v(ln);
-        if constexpr (NWG == 2) {
-            if (has_p) v_check_q<C>(sh, P_buf, P_off, P_n, wave, ln);
-            STAMP(7)
-        }
         if (cur_n > 0) {
             // c*'s snapshot coordinates (and exact distance), written by the wave that owns c*
-            if constexpr (NWG == 1)
-                write_cstar<C>(sh, creg, sh.qrec[cur_buf], (1ull << cur_n) - 1ull, 0, wave, ln, 0, trow);
+            write_cstar<C>(sh, creg, sh.qrec[cur_buf], (1ull << cur_n) - 1ull, 0, wave, ln, trow);
             STAMP(8)
 #pragma unroll 1
             for (int j0 = wave * 4; j0 < cur_n; j0 += 4 * NWL)
@@ -2043,15 +1844,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                     }
                 }
                 lds_barrier();
-                if constexpr (NWG == 2) {
-                    write_cstar<C>(sh, creg, sh.qrec[cur_buf], fx, 0, wave, ln, wg);
-                    lds_barrier();
-                    xchg_records<C>(sh, xp, nfx, sh.fxl, 0, sh.qrec[cur_buf], tid, wg);
-                    lds_barrier();
-                    fill_winner_coords<C>(sh, sh.qrec[cur_buf], nfx, sh.fxl, 0, tid, wg);
-                } else {
-                    write_cstar<C>(sh, creg, sh.qrec[cur_buf], fx, 0, wave, ln, 0, trow);
-                }
+                write_cstar<C>(sh, creg, sh.qrec[cur_buf], fx, 0, wave, ln, trow);
 #pragma unroll 1
                 for (int j0 = wave * 4; j0 < nfx; j0 += 4 * NWL)
                     a2_group<C, false>(sh, j0, nfx, sh.q[cur_buf], sh.qrec[cur_buf], 0, sh.fxl, ln);
@@ -2073,7 +1866,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             const int j = ln;
             const bool cj = j < k;
             const QRecT<D>& R = sh.qrec[P_buf][P_off + (cj ? j : 0)];
-            if (cj && wg0) {
+            if (cj) {
                 clusters[P_s + P_off + j] = R.id;
                 atomicAdd(&cnta[R.cstar], 1);
             }
@@ -2184,16 +1977,10 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             // gives ANN's answer whether or not a new certificate would pass
             // (41 % of the restarts on the C2 frame; the fresh A1 + A2 they skip
             // cost about 10k cycles each)
-            const bool snap_failed = NWG == 1 && uniform_int(sh.qrec[P_buf][P_off + fj].valid) == 0;
+            const bool snap_failed = uniform_int(sh.qrec[P_buf][P_off + fj].valid) == 0;
             if (!snap_failed) {
                 a1_query<C>(creg, sh.qslow, sh.wrec[vwave][KB], vwave, ln, dmask, trow, p0, tw_pass);
                 lds_barrier();
-                if constexpr (NWG == 2) {
-                    write_cstar<C>(sh, creg, &sh.qsolo, 1ull, KB, wave, ln, wg);
-                    lds_barrier();
-                    xchg_records<C>(sh, xp, 1, nullptr, KB, &sh.qsolo, tid, wg);
-                    lds_barrier();
-                }
                 if (wave == 0)
                     a2_group<C, false>(sh, 0, 1, reinterpret_cast<const float(*)[C::QD]>(sh.qslow), &sh.qsolo, KB,
                                        nullptr, ln);
@@ -2201,13 +1988,11 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             }
             int bpos;
             float key;
-            bool dfs = false;
             STAMP(10)
             if (!snap_failed && uniform_int(sh.qsolo.valid)) {
                 bpos = uniform_int(sh.qsolo.cstar);
                 key = sh.qsolo.g;
             } else {
-                dfs = true;
                 float dv[SL];
 #pragma unroll
                 for (int s = 0; s < SL; ++s) dv[s] = 0.0f;
@@ -2234,13 +2019,6 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
 #pragma unroll
                 for (int s = 0; s < SL; ++s)
                     if (p0 + s < K) sh.dist[p0 + s] = ((dmask >> s) & 1u) ? __builtin_inff() : dv[s];
-                if constexpr (NWG == 2) {  // the partner's half of the live distances
-                    lds_barrier();
-                    ++xp.seq;
-                    for (int i = tid; i < C::KG; i += nthreads) xput(xp, i, __float_as_uint(sh.dist[wg * C::KG + i]));
-                    for (int i = tid; i < C::KG; i += nthreads)
-                        sh.dist[(1 - wg) * C::KG + i] = __uint_as_float(xget(xp, i));
-                }
                 // the centroid registers stay live across the DFS (it needs ~40 more
                 // VGPRs; parking the 128 in C and reloading them cost 2x the DFS time)
                 lds_barrier();  // sh.dist complete
@@ -2259,8 +2037,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             }
             // owner publishes c's coordinates; tid 0 moves it (encoder.lpr:735-744);
             // the move enters the log (later batches' snapshots miss it) and the registers
-            const int owner = bpos >> LS, slot = bpos & (SL - 1);
-            const int owner_t = owner - wg * C::NT;  // owner thread within this workgroup
+            const int owner_t = bpos >> LS, slot = bpos & (SL - 1);  // owner thread
 #pragma unroll
             for (int s = 0; s < SL; ++s)
                 if (s == slot && tid == owner_t) {
@@ -2269,20 +2046,6 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                     if constexpr (C::SPLIT)
                         for (int d = C::DR; d < D; ++d) sh.solo_c[d] = trow[(int64_t)bpos * C::TL + (d - C::DR)];
                 }
-            if constexpr (NWG == 2) {
-                lds_barrier();
-                const int owg = bpos / C::KG;
-                if (dfs) {  // the owner's coordinates of c (any leaf)
-                    ++xp.seq;
-                    if (tid < D) xput(xp, tid, __float_as_uint(sh.solo_c[tid]));
-                    if (tid < D) {
-                        const float v = __uint_as_float(xget(xp, tid));
-                        if (owg != wg) sh.solo_c[tid] = v;
-                    }
-                } else if (owg != wg && tid < D) {  // the certified winner: received with the records
-                    sh.solo_c[tid] = sh.lw_p[KB][tid];
-                }
-            }
             lds_barrier();
             if (wave == kErrWave && ln == 0) err += (double)sqrt_rn(per_col(key));
             if (wave == 0) {
@@ -2292,10 +2055,8 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                         const float o = sh.solo_c[d];
                         sh.solo_c[d] = fadd(o, fmul(fsub(sh.qslow[d], o), rate));
                     }
-                    if (wg0) {
-                        atomicAdd(&cnta[bpos], 1);
-                        clusters[solo_j] = sh.t.pidx[bpos];
-                    }
+                    atomicAdd(&cnta[bpos], 1);
+                    clusters[solo_j] = sh.t.pidx[bpos];
                 }
                 wave_lds_sync();
                 const uint64_t hit = __ballot(lg_pos == bpos);
@@ -2314,11 +2075,11 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         }
         STAMP(5)
         if (nvq == 0 && cur_n == 0) {
-            if (tid == 0 && wg0) frp->loop_iters = it + 1;
+            if (tid == 0) frp->loop_iters = it + 1;
             break;
         }
         if (it > 4 * N + 64) {  // progress guard: every iteration commits or computes
-            if (tid == 0 && wg0) frp->loop_iters = -1;
+            if (tid == 0) frp->loop_iters = -1;
             guard = true;
             break;
         }
@@ -2338,21 +2099,20 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 for (int d = C::DR; d < D; ++d) C_[(int64_t)id * D + d] = trow[(int64_t)p * C::TL + (d - C::DR)];
         }
     }
-    if (wg0)
-        for (int p = tid; p < K; p += nthreads) {  // the commits' atomics live in L2: read past this CU's L1
-            const int id = sh.t.pidx[p];
-            if (id != 0xFFFF) prev_cnt[id] = __hip_atomic_load(&cnta[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+    for (int p = tid; p < K; p += nthreads) {  // the commits' atomics live in L2: read past this CU's L1
+        const int id = sh.t.pidx[p];
+        if (id != 0xFFFF) prev_cnt[id] = __hip_atomic_load(&cnta[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 #ifdef GSC_STAMPS
-    if (lane == 0 && wg0)
+    if (lane == 0)
         for (int k = 0; k < 16; ++k) frp->stamps[wave * 16 + k] += acc[k];
-    if (lane == 0 && wg0)
+    if (lane == 0)
         for (int k = 0; k < 8; ++k) frp->acounts[wave * 8 + k] += acn[k];
 #endif
     const double diff = err > prev_err ? err - prev_err : prev_err - err;
     const bool done = diff <= tol || pass + 1 >= kMaxScanIters || guard;
     prev_err = err;
-    if (tid == 0 && wg0) {
+    if (tid == 0) {
         frp->iters = pass + 1;
         frp->slow += slow_total;
         frp->restarts += restarts;
@@ -2361,18 +2121,13 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         if (done) frp->t_done = __builtin_amdgcn_s_memrealtime();  // diagnostic: the scan tail
     }
     // the next pass's tree build and rate lookups read C and prev_cnt as
-    // written above by other lanes (and, two-CU frames, by the partner)
-    if constexpr (NWG == 2) {
-        pair_barrier(xp, tid);
-        if (tid == 0 && wg0) frp->xseq = (int)xp.seq;
-    } else {
-        __threadfence();
-        __syncthreads();
-    }
+    // written above by other lanes
+    __threadfence();
+    __syncthreads();
     if (done) {
         // hand the final clusters to the host's post-processing while the
         // other frames still scan: a host-mapped copy, then the flag
-        int* clh = wg0 ? uniform_ptr(frp->cl_host) : nullptr;
+        int* clh = uniform_ptr(frp->cl_host);
         if (clh) {
             for (int j = tid; j < N; j += nthreads)
                 clh[j] = __hip_atomic_load(&clusters[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2392,65 +2147,48 @@ using namespace gsc;
 
 template <class C>
 static hipError_t launch_scan(ReduceFrame* frames, int nframes, const float* X, float* Cc, int* is,
-                              const float* rate_tab, double tol, int max_passes, uint64_t* xbuf, int opts,
-                              float* tails, hipStream_t st) {
+                              const float* rate_tab, double tol, int max_passes, int opts, float* tails,
+                              hipStream_t st) {
     const size_t shm = sizeof(Scan2Shared<C>);
     static_assert(sizeof(Scan2Shared<C>) <= 160 * 1024, "LDS budget (160 KB per CU)");
     hipError_t e = hipFuncSetAttribute((const void*)scan_batch_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)shm);
     if (e != hipSuccess) return e;
-    if constexpr (C::NWG == 1) {
-        hipLaunchKernelGGL(scan_batch_kernel<C>, dim3(nframes), dim3(C::NT), shm, st, frames, nframes, X, Cc, is,
-                           rate_tab, tol, max_passes, xbuf, opts, tails);
-        return hipGetLastError();
-    } else {
-        // both workgroups of a frame must be resident together: a cooperative
-        // grid of at most one workgroup per CU, frame pairs looping over frames
-        int dev = 0, cus = 0;
-        if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
-        if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
-        int pairs = std::min(nframes, std::max(1, cus / 2));
-        if (pairs >= 8) pairs -= pairs % 8;  // whole groups of 16 workgroups: pair members share an XCD
-        void* args[] = {&frames, &nframes, &X, &Cc, &is, &rate_tab, &tol, &max_passes, &xbuf, &opts, &tails};
-        return hipLaunchCooperativeKernel((const void*)scan_batch_kernel<C>, dim3(2 * pairs), dim3(C::NT), args, shm,
-                                          st);
-    }
+    hipLaunchKernelGGL(scan_batch_kernel<C>, dim3(nframes), dim3(C::NT), shm, st, frames, nframes, X, Cc, is, rate_tab,
+                       tol, max_passes, opts, tails);
+    return hipGetLastError();
 }
 
 // Batched KNNScanReduce for every frame (K <= 2^logk, 2^logk in 256..4096; a
-// frame's own K (frp->K) below 2^logk runs the padded layout; D = 8 or 16,
-// and D = 32 with two CUs per frame at K = 4096): each frame runs its passes
-// from frp->iters until it converges, reaches max_passes or meets a NaN pass
-// (left to the generic kernel).  xbuf: 2 x 2 x 2048 zeroed granules per frame
-// (D = 32, K = 4096 only).  Returns hipErrorInvalidValue for shapes it does
-// not cover.
+// frame's own K (frp->K) below 2^logk runs the padded layout; D = 8, 16 or 32,
+// D = 32 with K = 4096 in the split layout): each frame runs its passes from
+// frp->iters until it converges, reaches max_passes or meets a NaN pass (left
+// to the generic kernel).  Returns hipErrorInvalidValue for shapes it does not
+// cover.
 extern "C" hipError_t gsc_launch_scan_batch(int D, int logk, ReduceFrame* frames, int nframes, const float* X,
                                             float* Cc, int* is, const float* rate_tab, double tol, int max_passes,
-                                            uint64_t* xbuf, int opts, float* tails, hipStream_t st) {
-#define SB(DV, LK, SLV, NG)                                                                                    \
-    if (D == DV && logk == LK)                                                                                 \
-        return launch_scan<ScanCfg<DV, LK, SLV, NG>>(frames, nframes, X, Cc, is, rate_tab, tol, max_passes, xbuf, \
-                                                     opts, tails, st);
+                                            int opts, float* tails, hipStream_t st) {
+#define SB(DV, LK, SLV)                                                                                           \
+    if (D == DV && logk == LK)                                                                                    \
+        return launch_scan<ScanCfg<DV, LK, SLV>>(frames, nframes, X, Cc, is, rate_tab, tol, max_passes, opts, tails, \
+                                                 st);
     // K below 4096: fewer leaves per lane, so a frame keeps (up to) 8 waves --
     // the per-search work there is latency (A2 certificates, V checks and the
     // commit spread over the waves): K = 256 / 512 one leaf per lane (4 / 8
     // waves), K = 1024 two, K = 2048 four
-    SB(8, 8, 1, 1) SB(8, 9, 1, 1) SB(8, 10, 2, 1) SB(8, 11, 4, 1) SB(8, 12, 8, 1)
-    SB(16, 8, 1, 1) SB(16, 9, 1, 1) SB(16, 10, 2, 1) SB(16, 11, 4, 1) SB(16, 12, 8, 1)
-    SB(32, 8, 1, 1) SB(32, 9, 1, 1) SB(32, 10, 2, 1) SB(32, 11, 4, 1)
-    // D = 32, K = 4096: one CU per frame, the DCT half of every centroid in
-    // VGPRs and the cepstrum half in the frame's tail array (split layout;
-    // measured at D = 16 too: 4294 vs 4309 ms at the C2 bench shape, not kept)
+    SB(8, 8, 1) SB(8, 9, 1) SB(8, 10, 2) SB(8, 11, 4) SB(8, 12, 8)
+    SB(16, 8, 1) SB(16, 9, 1) SB(16, 10, 2) SB(16, 11, 4) SB(16, 12, 8)
+    SB(32, 8, 1) SB(32, 9, 1) SB(32, 10, 2) SB(32, 11, 4)
+    // D = 32, K = 4096: the DCT half of every centroid in VGPRs and the
+    // cepstrum half in the frame's tail array (split layout; measured at D = 16
+    // too: 4294 vs 4309 ms at the C2 bench shape, not kept)
     if (D == 32 && logk == 12)
-        return launch_scan<ScanCfg<32, 12, 8, 1, 16>>(frames, nframes, X, Cc, is, rate_tab, tol, max_passes, xbuf,
-                                                      opts, tails, st);
+        return launch_scan<ScanCfg<32, 12, 8, 16>>(frames, nframes, X, Cc, is, rate_tab, tol, max_passes, opts, tails,
+                                                   st);
 #undef SB
     return hipErrorInvalidValue;
 }
 
-extern "C" size_t gsc_scan_xbuf_granules_per_frame(void) { return 2 * 2 * (size_t)kXCap; }
-
-// floats of the split layout's tail array per frame (0: the shape keeps every feature in VGPRs)
 extern "C" size_t gsc_scan_tail_floats_per_frame(int D, int logk) {
     return logk == 12 && D == 32 ? 4096 * size_t(D / 2) : 0;
 }
