@@ -58,6 +58,7 @@ struct ReduceFrame {
     uint64_t stamps[128]; // out (GSC_STAMPS builds only): per-phase cycles, 16 per wave
     uint64_t ystamps[16]; // out (GSC_STAMPS builds only): yakmo phase cycles (gsc_yakmo.hip)
     uint64_t acounts[64]; // out (GSC_STAMPS builds only): per wave, A1 queries home / pruned / evaluated, iterations, fixups, pending size
+    uint64_t xcounts[16]; // out (GSC_STAMPS builds only, wave 0): iteration kinds and their cycles (gsc_scan.hip)
 };
 
 // One frame of the encoder's per-frame DSP: FindAttenuationDivider

@@ -271,7 +271,9 @@ hipError_t launch_scan_passes(int D, ReduceFrame* dfr, int nf, int K, const floa
         if (batched) {
             // opts bit 0 (diagnostic GSC_SCAN_FULL_A1): full-dimension A1 bounds in every pass
             // bit 1 (GSC_SCAN_NO_PRUNE, experiment): no per-wave A1 pruning
-            const int opts = (std::getenv("GSC_SCAN_FULL_A1") ? 1 : 0) | (std::getenv("GSC_SCAN_NO_PRUNE") ? 2 : 0);
+            // bits 8..15 (GSC_SCAN_KB, experiment): queries per speculative batch (below the kernel's 32)
+            const int opts = (std::getenv("GSC_SCAN_FULL_A1") ? 1 : 0) | (std::getenv("GSC_SCAN_NO_PRUNE") ? 2 : 0) |
+                             ((std::getenv("GSC_SCAN_KB") ? (std::atoi(std::getenv("GSC_SCAN_KB")) & 255) : 0) << 8);
             hipError_t e =
                 gsc_launch_scan_batch(D, logk, dfr, nf, X, C, is, rate, tol, max_passes, opts, tails.p, nullptr);
             if (e != hipSuccess) return e;
@@ -1831,6 +1833,13 @@ int gsc_scan_reduce(int n, int d0, const float* x, int k, float* centroids, int*
             std::fprintf(stderr, "\n  w%d:", w);
             for (int k = 0; k < 8; ++k) std::fprintf(stderr, " %.4g", double(fr[0].acounts[w * 8 + k]));
         }
+        const uint64_t* x = fr[0].xcounts;
+        std::fprintf(stderr,
+                     "\niterations [kind: count, cycles]: bubble %llu %.4g | with new queries %llu %.4g (new queries %llu)"
+                     " | with fixups %llu %.4g | with a solo %llu %.4g | A2 queries on per-wave bounds %llu",
+                     (unsigned long long)x[0], double(x[1]), (unsigned long long)x[2], double(x[3]),
+                     (unsigned long long)x[8], (unsigned long long)x[4], double(x[5]), (unsigned long long)x[6],
+                     double(x[7]), (unsigned long long)x[9]);
         std::fprintf(stderr, "\n");
     }
     return 0;

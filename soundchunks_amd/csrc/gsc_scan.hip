@@ -208,10 +208,13 @@ struct Scan2Shared {
     // per version: x = leaf position (-1 = none), y = first query that sees it,
     // z = last query that sees it (one 16-B read per version in the V check)
     alignas(16) int4 vmeta[C::KVER];
-    alignas(16) float newc[C::KB][C::ROW];
+    // new coordinates after each pending query's update and the next query with
+    // the same c*, by iteration parity: the waves fold from them after the
+    // commit decision while wave 0 may already run the next iteration's chain
+    alignas(16) float newc[2][C::KB][C::ROW];
     float gp[C::KB];       // live d(q_j, c*_j)
     int inval[C::KB];
-    int nxt[C::KB];        // next query of the batch with the same c* (KB = none)
+    int nxt[2][C::KB];     // next query of the batch with the same c* (KB = none), by iteration parity
     int ient[C::KB];       // log entry holding c*_j when the commit starts (-1 = none)
     int vie[C::KB];        // vp_begin: log entry holding c*_j (64 = none)
     int freel[64];         // commit: free log entries, in lane order
@@ -635,7 +638,7 @@ __device__ __forceinline__ void a2_group(Scan2Shared<C>& sh, int j0, int nq, con
                                          QRecT<C::D>* recs, int wcol0, const int* jlist, int lane,
                                          bool half = false, float twh = 0.0f, float te = 0.0f, bool nanpass = false
 #ifdef GSC_STAMPS
-                                         , uint64_t* acc = nullptr, uint64_t* tl = nullptr
+                                         , uint64_t* acc = nullptr, uint64_t* tl = nullptr, uint64_t* xc = nullptr
 #endif
 ) {
 #ifdef GSC_STAMPS
@@ -769,6 +772,9 @@ __device__ __forceinline__ void a2_group(Scan2Shared<C>& sh, int j0, int nq, con
         unique = fsub(__uint_as_float(m2), __uint_as_float(gmin)) > fadd(eps, eps);
         m2lo = fsub(fadd(qn, __uint_as_float(m2)), eps);
         const bool gfail = !unique || ((__ballot(!ok) >> gbase) & 0xFFFFull) != 0;
+#ifdef GSC_STAMPS
+        if (xc) xc[9] += __popcll(__ballot(gfail && l == 0 && qa));  // queries needing the per-wave bounds
+#endif
         if (__ballot(gfail) != 0) {
             // a query of this wave failed with the frame-wide bound: retry with an
             // error bound per wave.  A leaf of wave w has |c|^2 <= cnmax[w]
@@ -892,7 +898,7 @@ __device__ __forceinline__ void vp_begin(Scan2Shared<C>& sh, int qb, int off, in
 
 template <class C>
 __device__ __forceinline__ void vp_end(Scan2Shared<C>& sh, int qb, int off, int pn, int lane, int lg_pos,
-                                       const VPState& st) {
+                                       const VPState& st, bool half, int par) {
     constexpr int D = C::D, KB = C::KB;
     const int j = lane;
     const bool act = j < pn;
@@ -904,7 +910,7 @@ __device__ __forceinline__ void vp_end(Scan2Shared<C>& sh, int qb, int off, int 
     sh.vmeta[lane].z = lg_pos >= 0 ? st.first : -1;
     if (lane < KB) {
         sh.vmeta[64 + lane] = make_int4(act ? cs : -1, j + 1, act ? nxt : -1, 0);
-        sh.nxt[lane] = nxt;
+        sh.nxt[par][lane] = nxt;
         sh.ient[lane] = ie;
         sh.inval[lane] = 0;
     }
@@ -916,7 +922,7 @@ __device__ __forceinline__ void vp_end(Scan2Shared<C>& sh, int qb, int off, int 
         if (!rm) break;
         if (ready) {
             const float* qv = sh.q[qb][off + j];
-            const float* o = pred < 0 ? R.o : (pred < 64 ? sh.lg_c[pred] : sh.newc[pred - 64]);
+            const float* o = pred < 0 ? R.o : (pred < 64 ? sh.lg_c[pred] : sh.newc[par][pred - 64]);
             float oc[D];
 #pragma unroll
             for (int d = 0; d < D; ++d) oc[d] = o[d];
@@ -926,8 +932,14 @@ __device__ __forceinline__ void vp_end(Scan2Shared<C>& sh, int qb, int off, int 
             const float gpj = nanq ? __builtin_nanf("") : seqdist<D>(qv, oc);
             const bool okc = nanq || (R.valid != 0 && (pred < 0 || gpj < R.m2));
             const float rate = R.rate;
+            float nrm = 0.0f;  // |new c|^2 over the features the A1 bounds cover (norm2_x's order)
 #pragma unroll
-            for (int d = 0; d < D; ++d) sh.newc[j][d] = fadd(oc[d], fmul(fsub(qv[d], oc[d]), rate));
+            for (int d = 0; d < D; ++d) {
+                const float nc = fadd(oc[d], fmul(fsub(qv[d], oc[d]), rate));
+                sh.newc[par][j][d] = nc;
+                if (d < C::H || !half) nrm = __builtin_fmaf(nc, nc, nrm);
+            }
+            sh.newc[par][j][C::ROW - 1] = nrm;
             sh.gp[j] = gpj;
             if (!okc) sh.inval[j] = 1;
         }
@@ -936,66 +948,16 @@ __device__ __forceinline__ void vp_end(Scan2Shared<C>& sh, int qb, int off, int 
     }
 }
 
-// Commit, step 2 (all threads): every (query, moved centroid) pair of the
-// pending batch -- the moved centroid must stay provably outside ANN's answer.
-// Lane = query j (lane % KB); wave / lane group = a strided share of the
-// versions, so each version row is one LDS broadcast per group and the query
-// row stays in registers.  (Both workgroups of a two-CU frame check every pair.)
-template <class C>
-__device__ __forceinline__ void v_check_q(Scan2Shared<C>& sh, int qb, int off, int pn, int wave, int lane) {
-    constexpr int D = C::D, KB = C::KB, QPL = 64 / KB, LOGK = C::LOGK;
-    constexpr int VSTEP = QPL * C::NWL;  // versions apart between this lane group's consecutive versions
-    const int j = lane % KB, grp = lane / KB;
-    const int jr = j < pn ? j : 0;
-    const QRecT<D>& R = sh.qrec[qb][off + jr];
-    const bool act = j < pn && R.pad_ == 0;  // a NaN-first answer holds whatever moved
-    const int cs = R.cstar;
-    const uint32_t fm = R.farmask;
-    const float g = sh.gp[jr];
-    float q[D];
-#pragma unroll
-    for (int d = 0; d < D; ++d) q[d] = sh.q[qb][off + jr][d];
-    bool bad = false;
-    // two versions per trip, every LDS read of a trip issued before its
-    // arithmetic (metadata, both rows and the certificate thresholds B[lca]):
-    // one round trip of latency per two versions instead of three per version
-#pragma unroll 1
-    for (int v0 = wave * QPL + grp; v0 < C::KVER; v0 += 2 * VSTEP) {
-        const int v1 = v0 + VSTEP < C::KVER ? v0 + VSTEP : v0;
-        const bool h1 = v0 + VSTEP < C::KVER;
-        const int4 m0 = sh.vmeta[v0], m1 = sh.vmeta[v1];
-        const int vp0 = m0.x, vp1 = h1 ? m1.x : -1;
-        const bool u0 = (vp0 >= 0) & act & (j >= m0.y) & (j <= m0.z) & (vp0 != cs);
-        const bool u1 = (vp1 >= 0) & act & (j >= m1.y) & (j <= m1.z) & (vp1 != cs);
-        if (!(u0 || u1)) continue;
-        const float* c0 = v0 < 64 ? sh.lg_c[v0] : sh.newc[v0 - 64];
-        const float* c1 = v1 < 64 ? sh.lg_c[v1] : sh.newc[v1 - 64];
-        const int lca0 = __clz(vp0 ^ cs) - (32 - LOGK), lca1 = __clz(vp1 ^ cs) - (32 - LOGK);
-        const float b0 = R.B[lca0 & 15], b1 = R.B[lca1 & 15];  // in range whatever lca is; used only when u
-        float du0 = 0.0f, du1 = 0.0f;
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            const float t0 = fsub(q[d], c0[d]), t1 = fsub(q[d], c1[d]);
-            du0 = fadd(du0, fmul(t0, t0));
-            du1 = fadd(du1, fmul(t1, t1));
-        }
-        const bool far0 = (fm >> (lca0 & 31)) & 1u, far1 = (fm >> (lca1 & 31)) & 1u;
-        if (u0 && !(du0 > g && (!far0 || du0 > b0))) bad = true;
-        if (u1 && !(du1 > g && (!far1 || du1 > b1))) bad = true;
-    }
-    if (bad) sh.inval[j] = 1;
-}
-
 // The same checks as work items taken by whichever wave is free (one-CU
 // frames).  A1 is uneven across waves -- pruning leaves some waves a third of
 // the queries of others -- so the waves that finish A1 first run the V check
 // while the others still compute distances, instead of every wave doing an
 // eighth of it after the A1 barrier.  A trip = two versions per lane group
-// (as in v_check_q); the next trip's index is taken at the start of a trip
+// (lane = query, two versions per lane group); the next trip's index is taken at the start of a trip
 // (LDS atomic), and the checks start once wave 0's update chain (vp_end) of
 // this iteration is published (vp_ready).
 template <class C>
-__device__ __forceinline__ void v_check_grab(Scan2Shared<C>& sh, int qb, int off, int pn, int lane) {
+__device__ __forceinline__ void v_check_grab(Scan2Shared<C>& sh, int qb, int off, int pn, int lane, int par) {
     constexpr int D = C::D, KB = C::KB, QPL = 64 / KB, LOGK = C::LOGK;
     constexpr int VPT = 2 * QPL;  // versions per trip
     constexpr int NTRIP = (C::KVER + VPT - 1) / VPT;
@@ -1028,8 +990,8 @@ __device__ __forceinline__ void v_check_grab(Scan2Shared<C>& sh, int qb, int off
         const bool u0 = (vp0 >= 0) & act & (j >= m0.y) & (j <= m0.z) & (vp0 != cs);
         const bool u1 = (vp1 >= 0) & act & (j >= m1.y) & (j <= m1.z) & (vp1 != cs);
         if (u0 || u1) {
-            const float* c0 = v0s < 64 ? sh.lg_c[v0s] : sh.newc[v0s - 64];
-            const float* c1 = v1 < 64 ? sh.lg_c[v1] : sh.newc[v1 - 64];
+            const float* c0 = v0s < 64 ? sh.lg_c[v0s] : sh.newc[par][v0s - 64];
+            const float* c1 = v1 < 64 ? sh.lg_c[v1] : sh.newc[par][v1 - 64];
             const int lca0 = __clz(vp0 ^ cs) - (32 - LOGK), lca1 = __clz(vp1 ^ cs) - (32 - LOGK);
             const float b0 = R.B[lca0 & 15], b1 = R.B[lca1 & 15];
             float du0 = 0.0f, du1 = 0.0f;
@@ -1339,6 +1301,74 @@ __device__ __forceinline__ void refresh(Scan2Shared<C>& sh, float (&creg)[C::SL]
     if (lane == 0) sh.cnmax[vwave] = cnmax;
 }
 
+// fold the pending batch's committed updates (its first kc queries) into the
+// owners' registers, straight from the update chain's rows: query j carries
+// the last committed update of its c* when no later committed query of the
+// batch shares c* (the commit logs the same row, part 3)
+template <class C>
+__device__ __forceinline__ void fold_commits(Scan2Shared<C>& sh, float (&creg)[C::SL][C::DR], float (&cn)[C::SL],
+                                             float& cnmax, int vwave, int lane, int qb, int off, int kc, int par,
+                                             float* __restrict__ trow = nullptr) {
+    constexpr int SL = C::SL, LS = C::LS, D = C::D, DR = C::DR;
+    int pp = 0;
+    bool mine = false;
+    if (lane < kc) {
+        const QRecT<D>& R = sh.qrec[qb][off + lane];
+        pp = R.cstar;
+        mine = sh.nxt[par][lane] >= kc && R.pad_ == 0 && (pp >> (6 + LS)) == vwave;
+    }
+    uint64_t m = __ballot(mine);
+    if (!m) return;
+    float blo = __builtin_inff(), bhi = -__builtin_inff();  // lane d < D: the new positions' range
+    auto apply = [&](int e, int p, const float* r, float nv) {
+        const int owner = (p >> LS) & 63, slot = p & (SL - 1);
+#pragma unroll
+        for (int s = 0; s < SL; ++s) {
+            if (s == slot) {
+#pragma unroll
+                for (int d = 0; d < DR; ++d) creg[s][d] = lane == owner ? r[d] : creg[s][d];
+                cn[s] = lane == owner ? nv : cn[s];
+            }
+        }
+        if constexpr (C::SPLIT) {  // the owner's tail row (only the owner lane ever reads it)
+            if (lane == owner)
+                for (int d = DR; d < D; ++d) trow[(int64_t)p * C::TL + (d - DR)] = sh.newc[par][e][d];
+        }
+    };
+    // two rows per trip where the second fits the register budget (as refresh)
+    constexpr bool PAIR = DR <= 8;
+    while (m) {
+        const int e0 = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const bool two = PAIR && m != 0;
+        const int e1 = two ? __ffsll((long long)m) - 1 : e0;
+        if (two) m &= m - 1;
+        const int p0 = __builtin_amdgcn_readlane(pp, e0), p1 = __builtin_amdgcn_readlane(pp, e1);
+        float r0[DR], r1[PAIR ? DR : 1];
+#pragma unroll
+        for (int d = 0; d < DR; ++d) {
+            r0[d] = sh.newc[par][e0][d];
+            if constexpr (PAIR) r1[d] = sh.newc[par][e1][d];
+        }
+        const float nv0 = sh.newc[par][e0][C::ROW - 1], nv1 = sh.newc[par][e1][C::ROW - 1];  // |c|^2 (vp_end)
+        if (lane < D) {  // the pruning box covers the new positions
+            const float v0 = sh.newc[par][e0][lane], v1 = sh.newc[par][e1][lane];
+            blo = fminf(blo, fminf(v0, v1));
+            bhi = fmaxf(bhi, fmaxf(v0, v1));
+        }
+        cnmax = fmaxf(cnmax, fmaxf(nv0, nv1));  // only grows within a pass
+        apply(e0, p0, r0, nv0);
+        if constexpr (PAIR) {
+            if (two) apply(e1, p1, r1, nv1);
+        }
+    }
+    if (lane < D) {
+        sh.wlo[vwave][lane] = fminf(sh.wlo[vwave][lane], blo);
+        sh.whi[vwave][lane] = fmaxf(sh.whi[vwave][lane], bhi);
+    }
+    if (lane == 0) sh.cnmax[vwave] = cnmax;
+}
+
 // c*'s snapshot coordinates for the queries in qmask (columns col0 + j),
 // written by the lane that owns c* (the first wave / lane / slot at the
 // minimum of the A1 records, as in A2) into recs[j].o
@@ -1407,6 +1437,8 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     constexpr bool PRUNE = true;               // A1 pruning by wave boxes
     const bool no_half = (opts & 1) != 0;      // diagnostic: full-dimension A1 bounds in every pass
     const bool no_prune = (opts & 2) != 0;     // experiment: every wave evaluates every query (no mid-A1 barrier)
+    // experiment (opts bits 8..15): queries per speculative batch below KB
+    const int kbe = ((opts >> 8) & 255) > 0 && ((opts >> 8) & 255) < KB ? ((opts >> 8) & 255) : KB;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Scan2Shared<C>& sh = *reinterpret_cast<Scan2Shared<C>*>(smem);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1603,7 +1635,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         sh.vp_ready = 0;
     }
     // first batch's queries
-    const int n0 = min(KB, N);
+    const int n0 = min(kbe, N);
     for (int k = tid; k < n0 * D; k += nthreads) {
         const float x = X[k];
         sh.q[0][k / D][k % D] = x;
@@ -1664,6 +1696,9 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
 #ifdef GSC_STAMPS
     uint64_t acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t acn[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // home, pruned, evaluated, iterations, fixups, pending
+    // wave 0: bubble iterations / cycles, other iterations / cycles, iterations with fixups / cycles,
+    // iterations with a solo resolution / cycles, new queries, A2 queries needing per-wave bounds
+    uint64_t xc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tlast = stamp();
     acc[9] = tlast - t_kernel0;  // pass setup: tree build, registers, first queries
 #endif
@@ -1677,6 +1712,11 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     int next_load = n0;
     for (int it = 0;; ++it) {
         int ln = opaque_v(lane);  // see opaque_v: refreshed per phase below
+#ifdef GSC_STAMPS
+        const uint64_t t_it0 = stamp();
+        const bool it_bubble = cur_n == 0;  // no new batch: the remainder of a failed one is re-checked
+        bool it_fix = false;
+#endif
         const bool has_p = nvq > 0;
         const int P_buf = vq_buf0, P_s = vq_s0, P_off = vq_off0, P_n = has_p ? vq_n0 : 0;
         // ---- part 1: chain the pending batch's updates (wave 0); A1(current)
@@ -1692,7 +1732,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         constexpr bool kVpEarly = D <= 8;
         if constexpr (kVpEarly) {
             if (wave == 0 && has_p) {
-                vp_end<C>(sh, P_buf, P_off, P_n, ln, lg_pos, vst);
+                vp_end<C>(sh, P_buf, P_off, P_n, ln, lg_pos, vst, half, it & 1);
                 wave_lds_sync();
                 if (ln == 0) __hip_atomic_store(&sh.vp_ready, it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
@@ -1726,6 +1766,9 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             }
         };
         const uint64_t curm = cur_n > 0 ? (cur_n >= 64 ? ~0ull : (1ull << cur_n) - 1ull) : 0ull;
+#ifdef GSC_STAMPS
+        const int cur_n_it = cur_n;
+#endif
         uint64_t prunedm = 0;  // queries this wave skipped (wave-uniform)
         float lbp = 0.0f, qn_j = 0.0f, eps_j = 0.0f;  // ln j: query j's box bound, |q|^2, eps
         if constexpr (PRUNE) {
@@ -1779,7 +1822,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             a1_mask(curm);
         }
         if constexpr (!kVpEarly) {
-            if (wave == 0 && has_p) vp_end<C>(sh, P_buf, P_off, P_n, ln, lg_pos, vst);
+            if (wave == 0 && has_p) vp_end<C>(sh, P_buf, P_off, P_n, ln, lg_pos, vst, half, it & 1);
         }
         {
             STAMP(7)  // slot 7 = the rest of A1 (+ vp_end); slot 1 = the V check below
@@ -1794,7 +1837,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                     while (__hip_atomic_load(&sh.vp_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != it + 1)
                         __builtin_amdgcn_s_sleep(1);
                 }
-                v_check_grab<C>(sh, P_buf, P_off, P_n, ln);
+                v_check_grab<C>(sh, P_buf, P_off, P_n, ln, it & 1);
             }
         }
 #ifdef GSC_STAMPS
@@ -1804,109 +1847,26 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         STAMP(1)
         lds_barrier();
         STAMP(6)
-        // ---- part 2: check the pending batch; certificates of the current batch
-        ln = opaque_v(ln);
-        if (cur_n > 0) {
-            // c*'s snapshot coordinates (and exact distance), written by the wave that owns c*
-            write_cstar<C>(sh, creg, sh.qrec[cur_buf], (1ull << cur_n) - 1ull, 0, wave, ln, trow);
-            STAMP(8)
-#pragma unroll 1
-            for (int j0 = wave * 4; j0 < cur_n; j0 += 4 * NWL)
-                a2_group<C, true>(sh, j0, cur_n, sh.q[cur_buf], sh.qrec[cur_buf], 0, nullptr, ln, half, twh, te,
-                                  nan_rows != 0
-#ifdef GSC_STAMPS
-                                  , acc, &tlast
-#endif
-                );
-        }
-        STAMP(2)
-        lds_barrier();
-        if (cur_n > 0) {
-            // queries the approximate certificate could not decide: exact A1 + A2
-            // on the same snapshot (the registers change only in part 4)
-            const uint64_t fx = __ballot(ln < cur_n && sh.qrec[cur_buf][ln].valid == 0);
-            if (fx) {
-                const int nfx = __popcll(fx);
-#ifdef GSC_STAMPS
-                acn[4] += nfx;
-#endif
-                if (wave == 0 && ((fx >> ln) & 1ull)) sh.fxl[__popcll(fx & ((1ull << ln) - 1ull))] = ln;
-                uint64_t m = fx;
-                while (m) {
-                    const int jj = __ffsll((long long)m) - 1;
-                    m &= m - 1;
-                    if ((prunedm >> jj) & 1ull) {  // still provably far: the exact record's lower bound
-                        const float lb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbp), jj));
-                        if (ln == 0) sh.wrec[vwave][jj].minbits = __float_as_uint(lb);
-                    } else {
-                        a1_query<C>(creg, sh.q[cur_buf][jj], sh.wrec[vwave][jj], vwave, ln, dmask, trow, p0,
-                                    tw_pass);
-                    }
-                }
-                lds_barrier();
-                write_cstar<C>(sh, creg, sh.qrec[cur_buf], fx, 0, wave, ln, trow);
-#pragma unroll 1
-                for (int j0 = wave * 4; j0 < nfx; j0 += 4 * NWL)
-                    a2_group<C, false>(sh, j0, nfx, sh.q[cur_buf], sh.qrec[cur_buf], 0, sh.fxl, ln);
-                lds_barrier();
-            }
-        }
-        STAMP(3)
-        // ---- part 3: commit the valid prefix of the pending batch
+        // ---- part 2: commit decision (every wave: the V check is complete) and
+        // the next batch's queries, then the certificates of the current batch
+        // on the snapshot.  The registers must not change before the fixups:
+        // their exact records keep the pruning lower bounds of the waves that
+        // skipped a query, which hold for the snapshot only (with post-commit
+        // registers a pruned wave's bound could undercut every exact minimum
+        // and win the certificate with a record it never wrote).  So the fold
+        // follows the fixups, and the log bookkeeping and the residual run
+        // after them (part 3), all without the barrier the commit needed before
+        // (the fold reads the update chain's rows, not the log).
         ln = opaque_v(ln);
         int fj = -1;
         if (has_p) {
             const uint64_t bad = __ballot(ln < P_n && sh.inval[ln] != 0);
             fj = bad ? __ffsll((long long)bad) - 1 : -1;
         }
-        if (wave == kErrWave && has_p) {
-            // cluster ids, counts and the residual in query order (encoder.lpr:743:
-            // err += sqrt(best / colCount)) -- beside wave 0's log update
-            const int k = fj >= 0 ? fj : P_n;
-            const int j = ln;
-            const bool cj = j < k;
-            const QRecT<D>& R = sh.qrec[P_buf][P_off + (cj ? j : 0)];
-            if (cj) {
-                clusters[P_s + P_off + j] = R.id;
-                atomicAdd(&cnta[R.cstar], 1);
-            }
-            const float sq = cj ? sqrt_rn(per_col(sh.gp[j])) : 0.0f;
-#pragma unroll
-            for (int jj = 0; jj < KB; ++jj) {
-                const double t = (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(sq), jj));
-                err = jj < k ? err + t : err;
-            }
-        }
-        if (wave == 0 && has_p) {
-            const int k = fj >= 0 ? fj : P_n;
-            const int j = ln;
-            const bool cj = j < k;
-            const QRecT<D>& R = sh.qrec[P_buf][P_off + (cj ? j : 0)];
-            // the last committed update of each centroid becomes its log entry:
-            // the entry already holding that centroid, else the r-th free entry
-            const bool lastc = cj && sh.nxt[j] >= k && R.pad_ == 0;
-            int tgt = lastc ? sh.ient[j] : -1;
-            const uint64_t need = __ballot(lastc && tgt < 0);
-            const uint64_t freem = __ballot(lg_pos < 0);
-            const uint64_t below = (1ull << ln) - 1ull;
-            sh.asg[ln] = -1;
-            if (lg_pos < 0) sh.freel[__popcll(freem & below)] = ln;
-            wave_lds_sync();
-            if (lastc && tgt < 0) tgt = sh.freel[__popcll(need & below)];
-            if (lastc) {
-#pragma unroll
-                for (int d = 0; d < D; ++d) sh.lg_c[tgt][d] = sh.newc[j][d];
-                sh.lg_c[tgt][C::ROW - 1] = half ? norm2_x<C::H>(sh.newc[j]) : norm2_x<D>(sh.newc[j]);
-                sh.asg[tgt] = R.cstar;
-            }
-            wave_lds_sync();
-            const int a = sh.asg[ln];
-            if (a >= 0) {
-                lg_pos = a;
-                lg_tag = it;
-            }
-            if (fj >= 0 && ln < D) sh.qslow[ln] = sh.q[P_buf][P_off + fj][ln];
-        }
+        const int kc = has_p ? (fj >= 0 ? fj : P_n) : 0;  // committed prefix of the pending batch
+        if (wave == 0 && fj >= 0 && ln < D) sh.qslow[ln] = sh.q[P_buf][P_off + fj][ln];
+        // this iteration's current batch (certificates below); the queue moves on
+        const int A_buf = cur_buf, A_n = cur_n;
         // queue bookkeeping (uniform)
         const int solo_j = fj >= 0 ? P_s + P_off + fj : -1;
         if (has_p) {
@@ -1938,14 +1898,15 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             }
             ++nvq;
         }
-        // next batch of distances: into a free buffer, never the buffer a
-        // failed query's coordinates are being copied out of (wave 0, above)
+        // next batch of distances: into a free buffer (never the current batch's,
+        // whose certificates run below, nor the buffer a failed query's
+        // coordinates were copied out of, above)
         cur_n = 0;
         const int freeb = nvq == 0 ? (fj >= 0 ? P_buf ^ 1 : 0) : (nvq == 1 ? vq_buf0 ^ 1 : -1);
-        if (freeb >= 0 && !(fj >= 0 && freeb == P_buf) && next_load < N) {
+        if (freeb >= 0 && !(fj >= 0 && freeb == P_buf) && !(A_n > 0 && freeb == A_buf) && next_load < N) {
             cur_buf = freeb;
             cur_s = next_load;
-            cur_n = min(KB, N - next_load);
+            cur_n = min(kbe, N - next_load);
             next_load += cur_n;
 #pragma unroll
             for (int e = 0; e < PE; ++e) {
@@ -1957,16 +1918,109 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             }
         }
         if (tid == 0) sh.vc_next = 0;  // the next iteration's V check trips (taken after the A1 barrier)
-        if (wave == 0) {  // publish this iteration's commits (earlier ones are in the registers)
-            const bool fresh_e = lg_pos >= 0 && lg_tag == it;
-            sh.pub_pos[ln] = fresh_e ? lg_pos : -1;
-            if (PRUNE && ln < KB) sh.ub[ln] = kInfBits;  // the next batch's bounds
-        }
-        lds_barrier();
+        if (PRUNE && wave == 0 && ln < KB) sh.ub[ln] = kInfBits;  // the next batch's bounds
         STAMP(4)
-        // ---- part 4: fold the log into the registers
+        // ---- certificates of the current batch
+        if (A_n > 0) {
+            // c*'s coordinates, written by the wave that owns c*
+            write_cstar<C>(sh, creg, sh.qrec[A_buf], (1ull << A_n) - 1ull, 0, wave, ln, trow);
+            STAMP(8)
+#pragma unroll 1
+            for (int j0 = wave * 4; j0 < A_n; j0 += 4 * NWL)
+                a2_group<C, true>(sh, j0, A_n, sh.q[A_buf], sh.qrec[A_buf], 0, nullptr, ln, half, twh, te,
+                                  nan_rows != 0
+#ifdef GSC_STAMPS
+                                  , acc, &tlast, xc
+#endif
+                );
+        }
+        // the residual's terms and the cluster ids of the committed prefix, read
+        // before the barrier (wave 0 rewrites gp in the next iteration's update chain)
+        float err_sq = 0.0f;
+        if (wave == kErrWave && ln < kc) err_sq = sqrt_rn(per_col(sh.gp[ln]));
+        STAMP(2)
+        lds_barrier();
+        if (A_n > 0) {
+            // queries the approximate certificate could not decide: exact A1 + A2
+            // (on the registers as folded above)
+            const uint64_t fx = __ballot(ln < A_n && sh.qrec[A_buf][ln].valid == 0);
+            if (fx) {
+                const int nfx = __popcll(fx);
+#ifdef GSC_STAMPS
+                it_fix = true;
+                acn[4] += nfx;
+#endif
+                if (wave == 0 && ((fx >> ln) & 1ull)) sh.fxl[__popcll(fx & ((1ull << ln) - 1ull))] = ln;
+                uint64_t m = fx;
+                while (m) {
+                    const int jj = __ffsll((long long)m) - 1;
+                    m &= m - 1;
+                    if ((prunedm >> jj) & 1ull) {  // still provably far: the exact record's lower bound
+                        const float lb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbp), jj));
+                        if (ln == 0) sh.wrec[vwave][jj].minbits = __float_as_uint(lb);
+                    } else {
+                        a1_query<C>(creg, sh.q[A_buf][jj], sh.wrec[vwave][jj], vwave, ln, dmask, trow, p0,
+                                    tw_pass);
+                    }
+                }
+                lds_barrier();
+                write_cstar<C>(sh, creg, sh.qrec[A_buf], fx, 0, wave, ln, trow);
+#pragma unroll 1
+                for (int j0 = wave * 4; j0 < nfx; j0 += 4 * NWL)
+                    a2_group<C, false>(sh, j0, nfx, sh.q[A_buf], sh.qrec[A_buf], 0, sh.fxl, ln);
+                lds_barrier();
+            }
+        }
+        // every wave folds the committed updates of the centroids it owns, straight
+        // from the update chain's rows (no barrier after the commit decision)
+        if (kc > 0) fold_commits<C>(sh, creg, cn, cnmax, vwave, ln, P_buf, P_off, kc, it & 1, trow);
+        STAMP(3)
+        // ---- part 3: bookkeeping of the committed prefix
         ln = opaque_v(ln);
-        refresh<C>(sh, creg, cn, cnmax, vwave, ln, trow);
+        if (wave == kErrWave && has_p) {
+            // cluster ids, counts and the residual in query order (encoder.lpr:743:
+            // err += sqrt(best / colCount)) -- beside wave 0's log update
+            const int j = ln;
+            const bool cj = j < kc;
+            const QRecT<D>& R = sh.qrec[P_buf][P_off + (cj ? j : 0)];
+            if (cj) {
+                clusters[P_s + P_off + j] = R.id;
+                atomicAdd(&cnta[R.cstar], 1);
+            }
+#pragma unroll
+            for (int jj = 0; jj < KB; ++jj) {
+                const double t = (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(err_sq), jj));
+                err = jj < kc ? err + t : err;
+            }
+        }
+        if (wave == 0 && has_p) {
+            const int j = ln;
+            const bool cj = j < kc;
+            const QRecT<D>& R = sh.qrec[P_buf][P_off + (cj ? j : 0)];
+            // the last committed update of each centroid becomes its log entry:
+            // the entry already holding that centroid, else the r-th free entry
+            const bool lastc = cj && sh.nxt[it & 1][j] >= kc && R.pad_ == 0;
+            int tgt = lastc ? sh.ient[j] : -1;
+            const uint64_t need = __ballot(lastc && tgt < 0);
+            const uint64_t freem = __ballot(lg_pos < 0);
+            const uint64_t below = (1ull << ln) - 1ull;
+            sh.asg[ln] = -1;
+            if (lg_pos < 0) sh.freel[__popcll(freem & below)] = ln;
+            wave_lds_sync();
+            if (lastc && tgt < 0) tgt = sh.freel[__popcll(need & below)];
+            if (lastc) {
+#pragma unroll
+                for (int d = 0; d < D; ++d) sh.lg_c[tgt][d] = sh.newc[it & 1][j][d];
+                sh.lg_c[tgt][C::ROW - 1] = sh.newc[it & 1][j][C::ROW - 1];  // |c|^2 (vp_end)
+                sh.asg[tgt] = R.cstar;
+            }
+            wave_lds_sync();
+            const int a = sh.asg[ln];
+            if (a >= 0) {
+                lg_pos = a;
+                lg_tag = it;
+            }
+        }
         if (solo_j >= 0) {
             // the failed query on the live centroids: fresh distances and
             // certificate; exact DFS if the certificate still fails
@@ -2074,6 +2128,22 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             refresh<C>(sh, creg, cn, cnmax, vwave, ln, trow);
         }
         STAMP(5)
+#ifdef GSC_STAMPS
+        {
+            const uint64_t dt_ = stamp() - t_it0;
+            xc[it_bubble ? 0 : 2] += 1;
+            xc[it_bubble ? 1 : 3] += dt_;
+            if (it_fix) {
+                xc[4] += 1;
+                xc[5] += dt_;
+            }
+            if (solo_j >= 0) {
+                xc[6] += 1;
+                xc[7] += dt_;
+            }
+            xc[8] += (uint64_t)cur_n_it;
+        }
+#endif
         if (nvq == 0 && cur_n == 0) {
             if (tid == 0) frp->loop_iters = it + 1;
             break;
@@ -2108,6 +2178,8 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         for (int k = 0; k < 16; ++k) frp->stamps[wave * 16 + k] += acc[k];
     if (lane == 0)
         for (int k = 0; k < 8; ++k) frp->acounts[wave * 8 + k] += acn[k];
+    if (tid == 0)
+        for (int k = 0; k < 16; ++k) frp->xcounts[k] += xc[k];
 #endif
     const double diff = err > prev_err ? err - prev_err : prev_err - err;
     const bool done = diff <= tol || pass + 1 >= kMaxScanIters || guard;
