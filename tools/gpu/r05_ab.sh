@@ -18,4 +18,4 @@ for r in 1 2; do
   done
 done
 [ -n "$NOSTAMPS" ] && exit 0
-STCS="8 4" NOC4=1 bash tools/gpu/r05_stamps.sh
+STCS="8 4" bash tools/gpu/r05_stamps.sh
