@@ -1840,6 +1840,8 @@ int gsc_scan_reduce(int n, int d0, const float* x, int k, float* centroids, int*
                      (unsigned long long)x[0], double(x[1]), (unsigned long long)x[2], double(x[3]),
                      (unsigned long long)x[8], (unsigned long long)x[4], double(x[5]), (unsigned long long)x[6],
                      double(x[7]), (unsigned long long)x[9]);
+        std::fprintf(stderr, "\napproximate certificates failed: no unique minimum %llu, a far step not provable %llu",
+                     (unsigned long long)x[10], (unsigned long long)x[11]);
         std::fprintf(stderr, "\n");
     }
     return 0;

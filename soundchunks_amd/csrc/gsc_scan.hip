@@ -768,9 +768,33 @@ __device__ __forceinline__ void a2_group(Scan2Shared<C>& sh, int j0, int nq, con
         for (int w = 0; w < NW; ++w) M = fmaxf(M, sh.cnmax[w]);
         const float eps = fadd(fadd(fmul(fadd(qn0, M), C::EPSF), 1e-37f), te);
         const float qn = fadd(qn0, twh);  // the tail's midpoint (0 in full-dimension passes)
+#ifndef GSC_NO_LEAF_EPS
+        // Per-leaf error bounds.  The A1 value of a leaf c is within
+        // (|q|^2 + |c|^2) EPSF (+ TE) of the reference's distance -- the
+        // analysis above bounds every rounding by the leaf's own norms; M only
+        // stands in for |c|^2 -- and |c|^2 <= 2|q|^2 + 2|q - c|^2 with
+        // |q - c|^2 <= qn0 + v + 2 eg (v = the leaf's A1 value, eg = the
+        // frame-wide bound without TE; the factor 1 + 2^-20 covers this
+        // arithmetic).  So a leaf with A1 value v errs by at most epsv(v), and
+        // v - epsv(v) grows with v: bounds that hold for a subtree's minimum
+        // hold for all its leaves.  A quiet query among loud centroids (|q|^2,
+        // |q - c|^2 << M) gets its own scale instead of the loudest centroid's.
+        const float eg = fmul(fadd(qn0, M), C::EPSF);
+        auto epsv = [&](uint32_t vb) {
+            const float v = __uint_as_float(vb);
+            const float dq = fmaxf(fadd(fadd(qn0, v), fadd(eg, eg)), 0.0f);
+            const float cb = fmul(fadd(fadd(qn0, qn0), fadd(dq, dq)), 1.0f + 0x1p-20f);
+            return fadd(fadd(fmul(fadd(qn0, fminf(cb, M)), C::EPSF), 1e-37f), te);
+        };
+        const float es = epsv(gmin), e2 = epsv(m2), eb = epsv(sib);
+        ok = !far || (fsub(fadd(qn, __uint_as_float(sib)), eb) > Bv);
+        unique = fsub(__uint_as_float(m2), __uint_as_float(gmin)) > fadd(es, e2);
+        m2lo = fsub(fadd(qn, __uint_as_float(m2)), e2);
+#else
         ok = !far || (fsub(fadd(qn, __uint_as_float(sib)), eps) > Bv);
         unique = fsub(__uint_as_float(m2), __uint_as_float(gmin)) > fadd(eps, eps);
         m2lo = fsub(fadd(qn, __uint_as_float(m2)), eps);
+#endif
         const bool gfail = !unique || ((__ballot(!ok) >> gbase) & 0xFFFFull) != 0;
 #ifdef GSC_STAMPS
         if (xc) xc[9] += __popcll(__ballot(gfail && l == 0 && qa));  // queries needing the per-wave bounds
@@ -813,6 +837,12 @@ __device__ __forceinline__ void a2_group(Scan2Shared<C>& sh, int j0, int nq, con
     if (far && inc != inc) ok = false;  // a NaN box' is never visited (fmaxf would drop it from B)
     const bool gok = ((__ballot(!ok) >> gbase) & 0xFFFFull) == 0;
     const bool valid = unique && __uint_as_float(gmin) <= FLT_MAX && gok;
+#ifdef GSC_STAMPS
+    if (xc && APPROX) {  // why approximate certificates fail: no unique minimum / a far step not provable
+        xc[10] += __popcll(__ballot(qa && l == 0 && !unique));
+        xc[11] += __popcll(__ballot(qa && l == 0 && unique && !gok));
+    }
+#endif
     // NaN centroids (their leaves carry +inf in every distance here): ANN's DFS
     // reaches first the leaf of the near-child descent; a NaN leaf there becomes
     // the answer with key NaN (every later box' < NaN test fails) -- otherwise
