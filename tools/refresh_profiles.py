@@ -46,9 +46,20 @@ def main(rnd):
                            "bench.py --seconds 256 --steps 1 --warmup 0 (64 frames)"],
                           check=True, capture_output=True, text=True).stdout
     (out / "pmc_summary.json").write_text(summ)
-    line = [l for l in (PROF / "bench_default.log").read_text().splitlines() if l.startswith("{")][-1]
-    (out / "bench_1gpu.json").write_text(line + "\n")
-    print(json.loads(line)["value"])
+    if (PROF / "sq" / "run_results.db").exists():  # the SQ pass (tools/gpu/profile_r05.sh)
+        sql = [l for l in (PROF / "sq.log").read_text().splitlines() if l.startswith("{")][-1]
+        sqj = json.loads(sql)
+        summ = subprocess.run([sys.executable, str(ROOT / "tools/sq_summary.py"), str(PROF / "sq/run_results.db"),
+                               str(sqj["config"]["frames"]), str(sqj["scan"]["searches"]),
+                               "rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS "
+                               "SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_WAIT_ANY -- python3 bench.py --seconds 64 --steps 1 "
+                               f"--warmup 0 --no-cpu-baseline ({sqj['config']['frames']} C2 frames, MI355X, "
+                               "tools/gpu/profile_r05.sh)"], check=True, capture_output=True, text=True).stdout
+        (out / "pmc_sq_summary.json").write_text(summ)
+    if (PROF / "bench_default.log").exists():
+        line = [l for l in (PROF / "bench_default.log").read_text().splitlines() if l.startswith("{")][-1]
+        (out / "bench_1gpu.json").write_text(line + "\n")
+        print(json.loads(line)["value"])
 
 
 if __name__ == "__main__":
