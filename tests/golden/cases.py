@@ -73,6 +73,21 @@ def _silence_burst(seconds=3.0, rate=44100):
     return wav_header(1, rate, n) + np.round(x * 32767).astype("<i2").tobytes()
 
 
+def _square_empty_first(seconds=3.0, rate=44100):
+    """Mono full-scale square wave whose first sample is 0: every later sample
+    has power 1, so totalPower = 1 and at -cs4 (no padding) the cut loop ends
+    frame 0 at its first sample (encoder.lpr:1411-1417: curPower >= perFramePower
+    at i = 0), leaving frame 0 = (0, -1) -- one chunk (MakeChunks' ChunkCount =
+    (-1) div ChunkSize + 1) -- before one frame with the rest."""
+    from soundchunks_amd.synth import wav_header
+
+    n = int(seconds * rate)
+    t = np.arange(n) / rate
+    x = np.where(np.sin(2 * np.pi * 220 * t + 0.1) >= 0, 32767, -32767).astype(np.int64)
+    x[0] = 0
+    return wav_header(1, rate, n) + x.astype("<i2").tobytes()
+
+
 def _tiny():
     """0.02 s: fewer chunks than ChunksPerFrame -> passthrough mode (encoder.lpr:891-912)."""
     return _synth(0.02)
@@ -111,6 +126,16 @@ CASES = {
     "syn3s_cs3_mono_cbd12": (lambda: _synth(3.0, 44100, 1), ["-cs3", "-cpf1000", "-cbd12"]),
     "syn3s_cs6_cpf1024_cbd12": (lambda: _synth(3.0), ["-cs6", "-cpf1024", "-cbd12"]),
     "syn3s_cs12_cpf2048": (lambda: _synth(3.0), ["-cs12", "-cpf2048"]),
+    # ChunkSize 1 (2 features in the 8-wide kernels) and odd sizes in the 16-wide (5, 7) and
+    # 32-wide (9, 15) kernels: the odd-size sign / reverse split, the half-dimension tail box and
+    # the non-power-of-two residual divisor
+    "syn1s_cs1_cpf256": (lambda: _synth(1.0), ["-cs1", "-cpf256"]),
+    "syn2s_cs5_cpf512": (lambda: _synth(2.0), ["-cs5", "-cpf512"]),
+    "syn2s_cs7_mono_cbd12": (lambda: _synth(2.0, 44100, 1), ["-cs7", "-cpf1024", "-cbd12"]),
+    "syn2s_cs9_cpf512": (lambda: _synth(2.0), ["-cs9", "-cpf512"]),
+    "syn3s_cs15_cpf1024_cbd12": (lambda: _synth(3.0), ["-cs15", "-cpf1024", "-cbd12"]),
+    # an empty frame 0 = (0, -1) from the reference's cut, encoded (one chunk)
+    "square_empty_frame0_cs4": (lambda: _square_empty_first(), ["-cs4", "-cpf512"]),
     # a frame of more than 262,144 chunks (13-s frames at 48 kHz stereo -cs4: N ~ 312,000): yakmo's
     # chosen-point bitmap and prefix summaries live in HBM instead of LDS
     "syn13s_48k_cs4_cpf256_fl13000": (lambda: _synth(13.0, 48000), ["-cs4", "-cpf256", "-fl13000"]),

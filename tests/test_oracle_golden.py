@@ -237,3 +237,16 @@ def test_birch_host_part_matches_cluster_py(tmp_path, name):
     assert lib.birch_host_labels(x.shape[0], x.shape[1], ctypes.c_void_p(x.ctypes.data), int(z["k"]),
                                  ctypes.c_void_p(out.ctypes.data)) == 0
     np.testing.assert_array_equal(out, z["labels"])
+
+
+def test_oracle_frame_list_rejects_repeated_frames():
+    """ora_encode_frame_list refuses an index listed twice (two workers would
+    write the same frame's buffer) as it refuses one outside the file."""
+    import oracle_ffi
+    from soundchunks_amd.synth import synth_wav
+
+    wav = synth_wav(0.5)
+    with pytest.raises(RuntimeError, match="-2"):
+        oracle_ffi.encode_frame_list(wav, ["-cs8", "-cpf256"], [0, 0])
+    with pytest.raises(RuntimeError, match="-2"):
+        oracle_ffi.encode_frame_list(wav, ["-cs8", "-cpf256"], [5])
