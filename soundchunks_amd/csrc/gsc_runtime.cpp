@@ -1842,6 +1842,9 @@ int gsc_scan_reduce(int n, int d0, const float* x, int k, float* centroids, int*
                      double(x[7]), (unsigned long long)x[9]);
         std::fprintf(stderr, "\napproximate certificates failed: no unique minimum %llu, a far step not provable %llu",
                      (unsigned long long)x[10], (unsigned long long)x[11]);
+        std::fprintf(stderr, "\nfailed queries by cause: snapshot uncertified %llu, c* moved past m2 %llu, V check %llu"
+                     " (V check only %llu)", (unsigned long long)x[12], (unsigned long long)x[13],
+                     (unsigned long long)x[14], (unsigned long long)x[15]);
         std::fprintf(stderr, "\n");
     }
     return 0;

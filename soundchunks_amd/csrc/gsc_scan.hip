@@ -971,7 +971,11 @@ __device__ __forceinline__ void vp_end(Scan2Shared<C>& sh, int qb, int off, int 
             }
             sh.newc[par][j][C::ROW - 1] = nrm;
             sh.gp[j] = gpj;
+#ifdef GSC_STAMPS
+            if (!okc) sh.inval[j] = R.valid == 0 ? 1 : 2;  // cause (stamps): uncertified snapshot / c* moved past m2
+#else
             if (!okc) sh.inval[j] = 1;
+#endif
         }
         wave_lds_sync();  // this round's newc feed the next round's lanes
         done |= rm;
@@ -1037,7 +1041,11 @@ __device__ __forceinline__ void v_check_grab(Scan2Shared<C>& sh, int qb, int off
         }
         t = __builtin_amdgcn_readfirstlane(tn);
     }
+#ifdef GSC_STAMPS
+    if (bad) atomicOr(&sh.inval[j], 4);  // cause (stamps): a moved centroid broke the certificate
+#else
     if (bad) sh.inval[j] = 1;
+#endif
 }
 
 // Exact ANN ann_search (k = 1, eps = 0; annkSearch @0x1800124b0), all
@@ -1894,6 +1902,15 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             fj = bad ? __ffsll((long long)bad) - 1 : -1;
         }
         const int kc = has_p ? (fj >= 0 ? fj : P_n) : 0;  // committed prefix of the pending batch
+#ifdef GSC_STAMPS
+        if (fj >= 0) {  // why the first failing query failed
+            const int cause = sh.inval[fj];
+            xc[12] += (cause & 1) ? 1 : 0;
+            xc[13] += (cause & 2) ? 1 : 0;
+            xc[14] += (cause & 4) ? 1 : 0;
+            xc[15] += (cause & 4) && (cause & 3) == 0 ? 1 : 0;
+        }
+#endif
         if (wave == 0 && fj >= 0 && ln < D) sh.qslow[ln] = sh.q[P_buf][P_off + fj][ln];
         // this iteration's current batch (certificates below); the queue moves on
         const int A_buf = cur_buf, A_n = cur_n;
