@@ -134,6 +134,25 @@ __device__ __forceinline__ uint32_t wave_scan_u32(uint32_t x) {
     return x;
 }
 
+// f32 -> i32 as v_cvt_i32_f32 does it: saturating, NaN -> 0 (a C++ cast of
+// an out-of-range value would be undefined)
+__device__ __forceinline__ int cvt_sat_i32(float x) {
+    int r;
+    asm("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
+// Inclusive wave64 running max of non-negative integers (same DPP pattern)
+__device__ __forceinline__ int wave_max_scan(int x) {
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false));
+    return x;
+}
+
 // min / max over the 8 lanes of an aligned lane octet (DPP: quad_perm
 // [1,0,3,2], [2,3,0,1], then row_half_mirror across the two quads)
 __device__ __forceinline__ uint32_t oct_min_u32(uint32_t v) {
@@ -161,23 +180,28 @@ __device__ __forceinline__ uint32_t oct_max_u32(uint32_t v) {
 //
 // Points s .. s + 64 nbk - 1 of the ring (nbk <= 64 PPL / 64 blocks, s a
 // multiple of 64); lane l takes PPL consecutive points: one local prefix, one
-// wave scan.  The blocks before the first point that breaks a condition (tie,
-// |d/u| >= 2^24, a partial out of range) are accepted: their checkpoints and
-// min/max are written (global block index g0 + k) and *run_io moves to the
-// last accepted partial.  Returns the accepted block count.  run must be at
-// least 2^-100, so that 2^sc is a normal f32 and d * 2^sc is exact wherever
-// it matters (a d/u far below 1/2 may round: it still rounds to 0, no tie).
+// wave scan.  The blocks before the first lane holding a point that breaks a
+// condition (tie, |d/u| >= 2^24, NaN, a partial out of range) are accepted:
+// their checkpoints and min/max are written (global block index g0 + k) and
+// *run_io moves to the last accepted partial.  Returns the accepted block
+// count.  |run| must be at least 2^-100, so that 2^sc is a normal f32 and
+// d * 2^sc is exact wherever it matters (a d/u far below 1/2 may round: it
+// still rounds to 0, no tie); at run == 0 the leading blocks whose points are
+// all +-0 are accepted (fl(+0 + +-0) = +0: every partial stays +0).
+//
+// The check is per lane, on the lane's partials' min and max: lanes before
+// the first bad lane have every partial in range, so the first bad lane's
+// base is its exact predecessor partial; there a point with a tie or NaN
+// fails |t - rint(t)| < 1/2, and the first partial out of range is out of
+// range mod 2^32 as well (|n| < 2^24 + 2^23 would be needed to come back),
+// so the min or the max of the lane's base + partials (exact mod 2^32, as
+// int32) leaves [2^23 + 1, 2^24 - 2].
 template <int PPL>
 __device__ __forceinline__ int chain_fast(const float* __restrict__ ring, int s, int nbk, int lane, float* run_io,
                                           float* ck, float* bmn, float* bmx, int g0) {
     static_assert(PPL == 8 || PPL == 16, "8 or 16 points per lane");
     constexpr int LPB = 64 / PPL;  // lanes per 64-point block
     const float run = *run_io;
-    if (!(run >= 7.88860905e-31f)) return 0;  // below 2^-100, zero, negative (or NaN)
-    const int fe = __builtin_amdgcn_frexp_expf(run);  // run = f * 2^fe, f in [0.5, 1)
-    const int sc = 24 - fe;                          // d/u = d * 2^sc, sc <= 124
-    const float scale = __builtin_ldexpf(1.0f, sc), unscale = __builtin_ldexpf(1.0f, -sc);
-    const uint32_t m0 = (uint32_t)(run * scale);  // in [2^23, 2^24), exact
     const bool act = lane < nbk * LPB;
     float v[PPL];
     if (act) {
@@ -190,62 +214,138 @@ __device__ __forceinline__ int chain_fast(const float* __restrict__ ring, int s,
 #pragma unroll
         for (int e = 0; e < PPL; ++e) v[e] = 0.0f;
     }
-    uint32_t q[PPL], acc = 0;
-    bool ok[PPL];
+    // a negative run: the same on the negated points (round-to-nearest-even
+    // is odd-symmetric), partials m*u with m in [2^23, 2^24) from -run
+    const float arun = __builtin_fabsf(run);
+    if (!(arun >= 7.88860905e-31f)) {  // below 2^-100 in magnitude, zero (or NaN)
+        if (run != 0.0f) return 0;
+        bool nz = false;
+#pragma unroll
+        for (int e = 0; e < PPL; ++e) nz = nz || v[e] != 0.0f;  // NaN: != 0
+        const uint64_t bz = __ballot(act && nz);
+        const int k = bz ? min(nbk, __builtin_ctzll(bz) / LPB) : nbk;
+        const int blk = lane / LPB;
+        if (blk < k) {
+            if ((lane % LPB) == 0) bmn[g0 + blk] = bmx[g0 + blk] = 0.0f;
+            if ((lane % LPB) == LPB - 1) ck[g0 + blk] = 0.0f;
+        }
+        return k;  // run stays +0
+    }
+    const int fe = __builtin_amdgcn_frexp_expf(arun);  // |run| = f * 2^fe, f in [0.5, 1)
+    const int sc = 24 - fe;                           // d/u = d * 2^sc, sc <= 124
+    const float sgn = run < 0.0f ? -1.0f : 1.0f;
+    const float scale = sgn * __builtin_ldexpf(1.0f, sc), unscale = sgn * __builtin_ldexpf(1.0f, -sc);
+    const uint32_t m0 = (uint32_t)(run * scale);  // in [2^23, 2^24), exact
+    int n[PPL];
+    bool ok = true;
 #pragma unroll
     for (int e = 0; e < PPL; ++e) {
         const float t = v[e] * scale;
-        const float n = __builtin_rintf(t);
-        ok[e] = __builtin_fabsf(t) < 16777216.0f && __builtin_fabsf(t - n) != 0.5f;  // NaN: not ok
-        acc += (uint32_t)(int)n;  // garbage where !ok: that point fails below anyway
-        q[e] = acc;
+        const float r = __builtin_rintf(t);
+        ok = ok && __builtin_fabsf(t - r) < 0.5f;  // ties, NaN and infinities fail
+        n[e] = cvt_sat_i32(r);  // |t| >= 2^24 fails the range check
     }
-    // (a uint32 wrap needs an earlier partial out of range, which fails first)
-    const uint32_t base = m0 + (wave_scan_u32(acc) - acc);
-    uint64_t bad[PPL], anyb = 0;
+    // lane total as a tree, then the lane's partials from its base
+    uint32_t acc = 0;
+#pragma unroll
+    for (int e = 0; e < PPL; ++e) acc += (uint32_t)n[e];
+    const uint32_t p0 = m0 + (wave_scan_u32(acc) - acc);
+    uint32_t p = p0;
+    int mn = 0x7fffffff, mx = -0x7fffffff - 1;
 #pragma unroll
     for (int e = 0; e < PPL; ++e) {
-        q[e] += base;
-        // m + partial in [2^23 + 1, 2^24 - 2]: the exact sum, within 1/2 of
-        // it, lies strictly inside the binade and rounds on the grid u
-        bad[e] = __ballot(act && !(ok[e] && (q[e] - 8388609u) < 8388606u));
-        anyb |= bad[e];
+        p += (uint32_t)n[e];
+        mn = min(mn, (int)p);
+        mx = max(mx, (int)p);
     }
-    int k = nbk;
-    if (anyb) {
-        const int L = __builtin_ctzll(anyb);
-        int e0 = PPL - 1;
+    const uint64_t bl = __ballot(act && !(ok && mn >= 8388609 && mx <= 16777214));
+    int k = bl ? min(nbk, __builtin_ctzll(bl) / LPB) : nbk;
+#ifndef GSC_YAKMO_NO_TIES
+    if (k < nbk) {
+        // A tie t = j + 1/2 rounds to the even one of m + j, m + j + 1, with m
+        // the exact partial before it: rint(t) + c, c = 0 if m is even, else
+        // +1 (t - rint(t) = +1/2) or -1.  Each c != 0 flips the parity of all
+        // later partials, so the parity of the adjustments made up to and
+        // including tie i equals the parity b_i of the unadjusted (rint)
+        // partial at tie i, and c_i != 0 exactly when b_i != b_(i-1) (b_0 = 0).
+        // Two passes over the points, reloaded and re-rounded one at a time
+        // (nothing stays live across the first pass): the lanes' last tie
+        // parities, then the adjusted partials; t is clamped to 2^25 there,
+        // so the lane-relative partials stay below 2^30 and their min / max
+        // plus the lane base are exact.
+        const float4* row = reinterpret_cast<const float4*>(&ring[s + PPL * lane]);
+        uint32_t q = p0;
+        int key = 0;  // 2 lane + 1 + parity of the lane's last tie, 0: none
 #pragma unroll
-        for (int e = PPL - 1; e >= 0; --e)
-            if ((bad[e] >> L) & 1ull) e0 = e;
-        k = min(nbk, (L * PPL + e0) >> 6);
+        for (int h = 0; h < PPL / 4; ++h) {
+            const float4 a = act ? row[h] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            const float x4[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+            for (int l = 0; l < 4; ++l) {
+                const float t = x4[l] * scale;
+                const float r = __builtin_rintf(__builtin_amdgcn_fmed3f(t, -33554432.0f, 33554432.0f));
+                q += (uint32_t)cvt_sat_i32(r);
+                key = __builtin_fabsf(t - r) == 0.5f ? 2 * lane + 1 + (int)(q & 1u) : key;
+            }
+        }
+        if (__ballot(act && key != 0)) {
+            const int prev = __builtin_amdgcn_update_dpp(0, wave_max_scan(key), 0x138, 0xf, 0xf, false);  // wave_shr:1
+            uint32_t bprev = prev ? (uint32_t)(prev - 1) & 1u : 0u;
+            bool okt = true;
+            int rel = 0, rmn = 0x7fffffff, rmx = -0x7fffffff - 1, csum = 0;
+            q = p0;
+#pragma unroll
+            for (int h = 0; h < PPL / 4; ++h) {
+                const float4 a = act ? row[h] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                const float x4[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+                for (int l = 0; l < 4; ++l) {
+                    const float t = x4[l] * scale;
+                    const float r = __builtin_rintf(__builtin_amdgcn_fmed3f(t, -33554432.0f, 33554432.0f));
+                    const float dlt = t - r;
+                    const int ni = cvt_sat_i32(r);
+                    okt = okt && __builtin_fabsf(dlt) <= 0.5f;  // NaN and |t| > 2^25 fail
+                    q += (uint32_t)ni;
+                    const bool tie = __builtin_fabsf(dlt) == 0.5f;
+                    const uint32_t b = q & 1u;
+                    const int c = (tie && b != bprev) ? (dlt < 0.0f ? -1 : 1) : 0;
+                    bprev = tie ? b : bprev;
+                    csum += c;
+                    rel += ni + c;
+                    rmn = min(rmn, rel);
+                    rmx = max(rmx, rel);
+                }
+            }
+            const uint32_t base = p0 + (wave_scan_u32((uint32_t)csum) - (uint32_t)csum);
+            mn = (int)(base + (uint32_t)rmn);
+            mx = (int)(base + (uint32_t)rmx);
+            p = base + (uint32_t)rel;
+            const uint64_t b2 = __ballot(act && !(okt && mn >= 8388609 && mx <= 16777214));
+            k = b2 ? min(nbk, __builtin_ctzll(b2) / LPB) : nbk;
+        }
     }
+#endif
     if (k == 0) return 0;
-    uint32_t mn = q[0], mx = q[0];
-#pragma unroll
-    for (int e = 1; e < PPL; ++e) {
-        mn = min(mn, q[e]);
-        mx = max(mx, q[e]);
-    }
-    // in range, so integer order is the partials' order
+    // accepted lanes: in range, so integer order is the partials' order
     if constexpr (PPL == 8) {
-        mn = oct_min_u32(mn);
-        mx = oct_max_u32(mx);
+        mn = (int)oct_min_u32((uint32_t)mn);
+        mx = (int)oct_max_u32((uint32_t)mx);
     } else {
-        mn = min(mn, (uint32_t)__builtin_amdgcn_mov_dpp((int)mn, 0xb1, 0xf, 0xf, false));
-        mx = max(mx, (uint32_t)__builtin_amdgcn_mov_dpp((int)mx, 0xb1, 0xf, 0xf, false));
-        mn = min(mn, (uint32_t)__builtin_amdgcn_mov_dpp((int)mn, 0x4e, 0xf, 0xf, false));
-        mx = max(mx, (uint32_t)__builtin_amdgcn_mov_dpp((int)mx, 0x4e, 0xf, 0xf, false));
+        mn = min(mn, __builtin_amdgcn_mov_dpp(mn, 0xb1, 0xf, 0xf, false));
+        mx = max(mx, __builtin_amdgcn_mov_dpp(mx, 0xb1, 0xf, 0xf, false));
+        mn = min(mn, __builtin_amdgcn_mov_dpp(mn, 0x4e, 0xf, 0xf, false));
+        mx = max(mx, __builtin_amdgcn_mov_dpp(mx, 0x4e, 0xf, 0xf, false));
     }
     const int blk = lane / LPB;
     if (blk < k) {
         if ((lane % LPB) == 0) {
-            bmn[g0 + blk] = (float)mn * unscale;  // exact: < 2^24, same binade
-            bmx[g0 + blk] = (float)mx * unscale;
+            const float a = (float)mn * unscale, b = (float)mx * unscale;  // exact: < 2^24, same binade
+            bmn[g0 + blk] = fminf(a, b);  // (swapped for a negative run)
+            bmx[g0 + blk] = fmaxf(a, b);
         }
-        if ((lane % LPB) == LPB - 1) ck[g0 + blk] = (float)q[PPL - 1] * unscale;
+        if ((lane % LPB) == LPB - 1) ck[g0 + blk] = (float)p * unscale;
     }
-    *run_io = (float)(uint32_t)__builtin_amdgcn_readlane((int)q[PPL - 1], LPB * k - 1) * unscale;
+    *run_io = (float)(uint32_t)__builtin_amdgcn_readlane((int)p, LPB * k - 1) * unscale;
     return k;
 }
 

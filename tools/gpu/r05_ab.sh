@@ -13,7 +13,7 @@ for r in 1 2; do
     for cfg in ${CFGS:-c2:256 c5cs4:128}; do
       c=${cfg%%:*}; s=${cfg##*:}
       GSC_LIB=$(lib $v) timeout -k 10 300 python -u bench.py --config $c --seconds $s --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/ab_${v}_${c}_$r.log 2>&1 || exit 3
-      echo "$v $c $s r$r: $(tail -1 gpurun_out/ab_${v}_${c}_$r.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["stages_ms"]["gpu_scan_ms"], d["bit_exact"])')"
+      echo "$v $c $s r$r: $(tail -1 gpurun_out/ab_${v}_${c}_$r.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["stages_ms"]["gpu_yakmo_ms"], d["stages_ms"]["gpu_scan_ms"], d["bit_exact"])')"
     done
   done
 done
