@@ -49,7 +49,11 @@ __device__ __forceinline__ bool yakmo_idle_wave(int w) { return w == 4 || w == 8
 __device__ __forceinline__ int yakmo_dist_index(int w, int lane) { return (w - 1 - w / 4) * 64 + lane; }
 constexpr int kYMaxLds = 262144;      // frames up to this many points keep the yakmo state in LDS
 constexpr int kYBits = kYMaxLds / 32;  // chosen-point bitmap in LDS
-constexpr int kYPre = 3;              // d0 / seed-id prefetch depth (steps); X rows: 1
+#ifndef GSC_YAKMO_XD
+#define GSC_YAKMO_XD 1
+#endif
+constexpr int kYXD = GSC_YAKMO_XD;    // X-row look-ahead in steps
+constexpr int kYPre = kYXD == 1 ? 3 : 4;  // d0 / seed-id prefetch depth (steps), a multiple of kYXD
 
 #ifdef GSC_STAMPS
 // diagnostic phase clocks (make stamps): s_memtime deltas per role
@@ -533,7 +537,8 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
             for (int q = 0; q < kYPre; ++q)
 #pragma unroll
                 for (int p = 0; p < kYPts; ++p) {
-                    const int n = q * BLK + p * kYDist + dt;
+                    int n = q * BLK + p * kYDist + dt;
+                    asm volatile("" : "+v"(n));  // (no hoisted 64-bit address per slot)
                     pd[q][p] = 0.0f;
                     pa[q][p] = 0;
                     if (i > 0 && n < N) {
@@ -636,8 +641,9 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
             // pipeline: step b computes block b (kYPts points per thread, kYDist
             // apart); the X rows of block b + XD (when not skipped) and the d0 /
             // seed ids of block b + kYPre are loaded meanwhile
-            constexpr int XD = 1;  // X-row look-ahead in steps (a step is 1024 points)
+            constexpr int XD = kYXD;  // X-row look-ahead in steps (a step is 1024 points)
             float xv[XD][kYPts][D];
+            float xnv[XD][kYPts];  // yakmo's |x|^2 (norm[], computed at the start)
             bool skip[XD][kYPts];
 #pragma unroll
             for (int q = 0; q < XD; ++q)
@@ -648,6 +654,7 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
                     if (n < N) {
                         skip[q][p] = skip_of(pd[q][p], pa[q][p]);
                         if (!skip[q][p]) {
+                            xnv[q][p] = norm[n];
 #pragma unroll
                             for (int j = 0; j < D; ++j) xv[q][p][j] = X[(int64_t)n * D + j];
                         }
@@ -665,10 +672,7 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
                         if (b < nblk && n < N) {
                             float dn = pd[u][p];
                             if (!skip[s2][p]) {
-                                float xn = 0.0f;  // yakmo's |x|^2, as computed at the start
-#pragma unroll
-                                for (int j = 0; j < D; ++j) xn = fa(xn, fm(xv[s2][p][j], xv[s2][p][j]));
-                                float d = fa(fa(cn, xn), 0.0f);
+                                float d = fa(fa(cn, xnv[s2][p]), 0.0f);
 #pragma unroll
                                 for (int j = 0; j < D; ++j) d = fs(d, fm(fa(xv[s2][p][j], xv[s2][p][j]), c[j]));
                                 if (i == 0 || dn > d) {
@@ -690,6 +694,7 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
                         if (b + XD < nblk && n2 < N) {
                             skip[s2][p] = skip_of(pd[(u + XD) % kYPre][p], pa[(u + XD) % kYPre][p]);
                             if (!skip[s2][p]) {
+                                xnv[s2][p] = norm[n2];
 #pragma unroll
                                 for (int j = 0; j < D; ++j) xv[s2][p][j] = X[(int64_t)n2 * D + j];
                             }
