@@ -615,6 +615,7 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
             const float cmax = sh.cmax, xmax = sh.xmax;
             // Seed-distance table: sdlo[a] <= |c_i - c_a|^2 (the f32 sum of squared
             // differences, lowered by 2^-16 relative to cover its rounding).
+#pragma unroll 4  // (up to four rows' loads in flight before their sums)
             for (int a = dt; a < i; a += kYDist) {
                 float s2 = 0.0f;
 #pragma unroll
