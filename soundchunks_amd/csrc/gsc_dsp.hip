@@ -268,6 +268,7 @@ using namespace gsc;
 
 extern "C" hipError_t gsc_launch_pcm(const int16_t* pcm, int64_t span, int ch, double* samp, hipStream_t st) {
     const int64_t total = span * ch;
+    if (total <= 0) return hipSuccess;  // an empty span (a frame (0, -1): encoder.lpr:1411-1417)
     const int64_t blocks = (total + 255) / 256;
     hipLaunchKernelGGL(pcm_kernel, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, st, pcm, span, ch,
                        samp);
@@ -299,6 +300,7 @@ extern "C" hipError_t gsc_launch_atten(int cs, DspFrame* frames, int nframes, co
 extern "C" hipError_t gsc_launch_features(int cs, const DspFrame* frames, int nframes, int max_n, const double* samp,
                                           int64_t span, int ch, const double* trig, double s0, double scale, float* X,
                                           uint8_t* nr, float* Q, hipStream_t st) {
+    if (max_n <= 0 || nframes <= 0) return hipSuccess;
     const dim3 grid((max_n + 255) / 256, nframes), block(256);
     switch (cs) {
 #define FK(CSV)                                                                                                  \

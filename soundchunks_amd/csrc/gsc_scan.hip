@@ -1223,38 +1223,88 @@ __device__ __noinline__ void dfs_parallel_nan(Scan2Shared<C>& sh, int tid, int l
         }
     }
     lds_barrier();
+    // The paths do not depend on the improvement round, only the choice of
+    // far steps does: with the leaf's DFS rank R > pos and t the highest bit
+    // where R and pos differ, the far steps with start > pos are exactly those
+    // at levels >= LOGK - 1 - t.  So each path is walked once, keeping the
+    // suffix maxima of box' by level (NaN = +inf): shared over the thread's
+    // top LOGK - 3 levels, per leaf over the last three.
     const int p0 = tid * 8;
-    auto far_step = [&](int h, int bit, int l, float& box, float& M, int& pref, int pos) {
-        const int nearbit = ((sh.dfs_near[h >> 5] >> (h & 31)) & 1u) ? 0 : 1;
-        if (bit != nearbit) {  // the leaf lies in the far child: its subtree starts after the near one
-            box = fadd(box, sh.dfs_inc[h]);
-            pref += 1 << (LOGK - 1 - l);
-            if (pref > pos) M = box != box ? __builtin_inff() : fmaxf(M, box);
+    constexpr int LT = LOGK - 3;  // shared levels
+    float smt[LT + 1];            // suffix max of the shared far boxes from level l
+    int preft = 0;                // rank prefix of the thread's 8 leaves
+    float boxt = rootbox;
+    int ht = 0;
+    {
+        float fb[LT];
+#pragma unroll
+        for (int l = 0; l < LT; ++l) {
+            const int bit = (p0 >> (LOGK - 1 - l)) & 1;
+            const int nearbit = ((sh.dfs_near[ht >> 5] >> (ht & 31)) & 1u) ? 0 : 1;
+            fb[l] = -__builtin_inff();
+            if (bit != nearbit) {  // the leaf lies in the far child: its subtree starts after the near one
+                boxt = fadd(boxt, sh.dfs_inc[ht]);
+                preft += 1 << (LOGK - 1 - l);
+                fb[l] = boxt != boxt ? __builtin_inff() : boxt;
+            }
+            ht = 2 * ht + 1 + bit;
         }
-    };
+        smt[LT] = -__builtin_inff();
+#pragma unroll
+        for (int l = LT - 1; l >= 0; --l) smt[l] = fmaxf(fb[l], smt[l + 1]);
+    }
+    int rk[8];        // the leaves' DFS ranks
+    float sb[8][3];   // per leaf: suffix max of its own far boxes from level LT + j
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8) {
+        float box = boxt, fb[3];
+        int pref = preft, h = ht;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int l = LT + j;
+            const int bit = ((p0 + s8) >> (LOGK - 1 - l)) & 1;
+            const int nearbit = ((sh.dfs_near[h >> 5] >> (h & 31)) & 1u) ? 0 : 1;
+            fb[j] = -__builtin_inff();
+            if (bit != nearbit) {
+                box = fadd(box, sh.dfs_inc[h]);
+                pref += 1 << (LOGK - 1 - l);
+                fb[j] = box != box ? __builtin_inff() : box;
+            }
+            h = 2 * h + 1 + bit;
+        }
+        rk[s8] = pref;
+        sb[s8][2] = fb[2];
+        sb[s8][1] = fmaxf(fb[1], fb[2]);
+        sb[s8][0] = fmaxf(fb[0], sb[s8][1]);
+    }
     int pos = -1, bp = -1, par = 0;
     float b = FLT_MAX;  // the empty list's max_key
     for (;;) {
-        float box = rootbox, M = -__builtin_inff();
-        int pref = 0, h = 0;
-        for (int l = 0; l < LOGK - 3; ++l) {
-            const int bit = (p0 >> (LOGK - 1 - l)) & 1;
-            far_step(h, bit, l, box, M, pref, pos);
-            h = 2 * h + 1 + bit;
-        }
         uint32_t key = 0xFFFFFFFFu;
+        const int gt = preft >> 3, gp = pos >> 3;  // (pos = -1: gp = -1)
+        if (gt > gp) {  // every leaf of the thread ranks after pos; t >= 3
+            const int t = 31 - __builtin_clz((uint32_t)(preft ^ pos));
+            const int lt = max(0, LOGK - 1 - t);
+            float mt = smt[0];
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            float box2 = box, M2 = M;
-            int pref2 = pref, h2 = h;
+            for (int l = 1; l < LT; ++l) mt = l == lt ? smt[l] : mt;
 #pragma unroll
-            for (int l = LOGK - 3; l < LOGK; ++l) {
-                const int bit = ((p0 + s) >> (LOGK - 1 - l)) & 1;
-                far_step(h2, bit, l, box2, M2, pref2, pos);
-                h2 = 2 * h2 + 1 + bit;
+            for (int s8 = 0; s8 < 8; ++s8) {
+                const float M = fmaxf(mt, sb[s8][0]);
+                if (p0 + s8 < K && M < b && sh.dist[p0 + s8] < b)
+                    key = min(key, ((uint32_t)rk[s8] << 12) | (uint32_t)(p0 + s8));
             }
-            if (p0 + s < K && pref2 > pos && M2 < b && sh.dist[p0 + s] < b)
-                key = min(key, ((uint32_t)pref2 << 12) | (uint32_t)(p0 + s));
+        } else if (gt == gp) {  // pos inside the thread's group: only the last three levels choose
+#pragma unroll
+            for (int s8 = 0; s8 < 8; ++s8) {
+                const int x = (rk[s8] ^ pos) & 7;
+                if (rk[s8] > pos && x != 0) {
+                    const int t = 31 - __builtin_clz((uint32_t)x);  // 0..2
+                    const float M = t == 2 ? sb[s8][0] : (t == 1 ? sb[s8][1] : sb[s8][2]);
+                    if (p0 + s8 < K && M < b && sh.dist[p0 + s8] < b)
+                        key = min(key, ((uint32_t)rk[s8] << 12) | (uint32_t)(p0 + s8));
+                }
+            }
         }
         key = min(key, partner<0>(key));
         key = min(key, partner<1>(key));

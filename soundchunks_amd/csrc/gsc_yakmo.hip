@@ -579,6 +579,11 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
             YST(3)
             // sequential f32 prefix over the blocks as they complete (encoder's cum[], DLL @0x180001e74)
             float run = 0.0f;
+            // back-off: after consecutive fast-path calls that accept nothing
+            // (a total hovering around zero in quiet real audio changes binade
+            // at nearly every point), the next 1, 3, 7, 15 blocks go point by
+            // point without trying
+            int fails = 0, skipfast = 0;
             for (int b = 0; b <= nblk; ++b) {
                 if (chain && b > 0) {
                     const int base = (b - 1) * BLK;
@@ -587,11 +592,16 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
                     int s = 0;
                     while (s < cnt) {
                         const int full = (cnt - s) >> 6;
-                        if (full > 0) {
+                        if (full > 0 && skipfast == 0) {
                             const int k = chain_fast<BLK / 64>(rg, s, full, lane, &run, ck, bmn, bmx, (base + s) >> 6);
                             s += k << 6;
+                            fails = k > 0 ? 0 : min(fails + 1, 5);
+                            skipfast = (1 << fails) >> 1;
+                            skipfast = skipfast > 0 ? skipfast - 1 : 0;
                             YST(1) YCNT(4)
                             if (s >= cnt) break;
+                        } else if (skipfast > 0) {
+                            --skipfast;
                         }
                         // the block at s breaks a fast-path condition (or is the last, partial one)
                         const int c = min(64, cnt - s);
