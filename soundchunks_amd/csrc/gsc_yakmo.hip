@@ -593,7 +593,12 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
                     while (s < cnt) {
                         const int full = (cnt - s) >> 6;
                         if (full > 0 && skipfast == 0) {
-                            const int k = chain_fast<BLK / 64>(rg, s, full, lane, &run, ck, bmn, bmx, (base + s) >> 6);
+                            // (at most 8 blocks left, e.g. after a break: 8 points per lane)
+                            int k;
+                            if (BLK / 64 == 16 && full <= 8)
+                                k = chain_fast<8>(rg, s, full, lane, &run, ck, bmn, bmx, (base + s) >> 6);
+                            else
+                                k = chain_fast<BLK / 64>(rg, s, full, lane, &run, ck, bmn, bmx, (base + s) >> 6);
                             s += k << 6;
                             fails = k > 0 ? 0 : min(fails + 1, 5);
                             skipfast = (1 << fails) >> 1;
