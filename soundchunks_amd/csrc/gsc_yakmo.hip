@@ -265,7 +265,10 @@ __device__ __forceinline__ int chain_fast(const float* __restrict__ ring, int s,
     const uint64_t bl = __ballot(act && !(ok && mn >= 8388609 && mx <= 16777214));
     int k = bl ? min(nbk, __builtin_ctzll(bl) / LPB) : nbk;
 #ifndef GSC_YAKMO_NO_TIES
-    if (k < nbk) {
+    // (only when the first failing lane itself holds a tie, NaN or infinity:
+    // a lane that fails on range alone has no tie, and the lanes before it
+    // none either, so resolving ties cannot move k -- a binade crossing)
+    if (k < nbk && __builtin_amdgcn_readlane((int)ok, __builtin_ctzll(bl)) == 0) {
         // A tie t = j + 1/2 rounds to the even one of m + j, m + j + 1, with m
         // the exact partial before it: rint(t) + c, c = 0 if m is even, else
         // +1 (t - rint(t) = +1/2) or -1.  Each c != 0 flips the parity of all
