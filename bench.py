@@ -254,6 +254,11 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="all-core CPU baseline threads (default: the job's CPU share, cgroup quota or affinity)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--share", default=None, metavar="R/N",
+                    help="--strong on one GPU: encode only rank R of N's frame range of the whole file (the "
+                         "PrepareFrames cut of the whole file, the range an N-GPU run gives rank R)")
+    ap.add_argument("--dist", action="store_true",
+                    help="run the torch.distributed path (bounds broadcast, all-gather) even at --gpus 1")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo rehearses the "
                          "multi-rank path on host tensors, e.g. 2 ranks on a one-GPU box)")
@@ -262,6 +267,12 @@ def main():
         args.cpu_threads = _cpu_share()[0]
 
     ws, rank, local = _dist_env()
+    share = None
+    if args.share:
+        share = tuple(int(v) for v in args.share.split("/"))
+        if not (args.strong and args.gpus == 1 and len(share) == 2 and 0 <= share[0] < share[1]):
+            print("bench.py: --share R/N needs --strong, --gpus 1 and 0 <= R < N", file=sys.stderr)
+            sys.exit(2)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         from soundchunks_amd.shard import spawn_workers
 
@@ -279,16 +290,25 @@ def main():
     gpu = local % max(1, torch.cuda.device_count())
     dev = torch.device("cuda", gpu)
     cdev = dev if args.backend == "nccl" else torch.device("cpu")  # where the collectives' tensors live
-    if ws > 1:
+    # the collective path runs for N > 1, and at N = 1 under a launcher
+    # (WORLD_SIZE in the environment) or with --dist: a one-rank RCCL group
+    # executes the same broadcast / all-gather code an N-GPU run takes
+    use_dist = ws > 1 or "WORLD_SIZE" in os.environ or args.dist
+    if use_dist:
         import torch.distributed as dist
 
+        if "WORLD_SIZE" not in os.environ:  # --dist alone: a one-rank group at 127.0.0.1
+            from soundchunks_amd.shard import free_port
+
+            os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+                              MASTER_PORT=str(free_port()))
         torch.cuda.set_device(gpu)
         dist.init_process_group(args.backend)
     import soundchunks_amd as sc
     from soundchunks_amd.shard import bounds_range, broadcast_bounds, gather_streams
     from soundchunks_amd.synth import synth_wav
 
-    if ws > 1:
+    if use_dist:
         sc.set_device(gpu)
 
     argv, ch, rate, cs, desc = CONFIGS[args.config]
@@ -319,8 +339,9 @@ def main():
                 nxt = pool.submit(prepare_job)
         if dist is not None:  # rank 0's PrepareFrames boundaries to every rank
             st, en = broadcast_bounds(st, en, device=cdev)
-        b, e = bounds_range(st, en, cs, ch, rank, ws)
+        b, e = bounds_range(st, en, cs, ch, *(share or (rank, ws)))
         info["frames"], info["range"] = len(st), (b, e)
+        info["range_samples"] = int(sum(int(en[f]) - int(st[f]) + 1 for f in range(b, e))) * ch
         t_enc = time.perf_counter()
         if rank == 0:
             out, sizes = p.encode_frames(b, e)
@@ -380,15 +401,23 @@ def main():
         if bad:
             sys.exit(3)
         return
-    if listed == info["frames"] and checked == listed:
+    if share is None and listed == info["frames"] and checked == listed:
         want_len = json.loads(DIGESTS.read_text())[key].get("total_bytes")
         if want_len is not None and len(whole) != int(want_len):
             bad += 1
     n_samples = int(round(total_seconds * rate)) * ch
+    if share is not None:  # one rank's share: the samples of its frames
+        n_samples = info["range_samples"]
     value = n_samples * args.steps / dt / 1e6
     result = base_result(args, ws, dt, value, desc, enc, timings[-1], cs, argv, rate, ch)
     result["config"] = {"workload": f"{desc}, {total_seconds:g} s synthetic", "frames": info["frames"],
-                        "argv": argv, "parallelism": f"frame-sharded x{ws}", "rank0_frames": list(info["range"])}
+                        "argv": argv, "parallelism": f"frame-sharded x{ws}", "rank0_frames": list(info["range"]),
+                        "collectives": args.backend if dist is not None else None}
+    if share is not None:
+        result["config"]["share"] = {"rank": share[0], "of": share[1], "frames": list(info["range"]),
+                                     "samples": n_samples,
+                                     "note": "rank R of N's frame range of the whole file's PrepareFrames cut, "
+                                             "encoded alone on one GPU (prepare of the whole file included)"}
     result["data"] = (f"synthetic (SURVEY.md §8d tone+noise, PCG64 20250217), "
                       f"{total_seconds:g} s {'in total' if args.strong else f'= {args.seconds:g} s per GPU'}")
     result["prepare_ms"] = round(info["prepare_ms"], 1)
@@ -399,6 +428,7 @@ def main():
         "digests": f"tests/golden/bench_digests.json[{key}] (oracle SaveStream bytes per frame)",
         "frames_checked": checked, "frames_differing": bad, "frames_total": info["frames"],
         "whole_file": checked == info["frames"],
+        "range_checked": checked == info["range"][1] - info["range"][0],
         "note": None if checked else "no oracle digests for this workload: not checked"}
     if not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.config, argv, rate, ch, enc.frame_length / 1000.0,
@@ -524,7 +554,7 @@ def bench_corpus(args, enc, argv, desc, ws, rank, cdev, dist, cs):
     result = base_result(args, ws, dt, value, desc, enc, tm, cs, argv, 44100, 1)
     result["config"] = {"workload": f"{desc}, {n_samples / 44100:.1f} s of audio in {len(wavs)} files",
                         "files": len(wavs), "frames": tm["frames"], "argv": argv,
-                        "parallelism": f"frame-sharded x{ws}"}
+                        "parallelism": f"frame-sharded x{ws}", "collectives": args.backend if dist is not None else None}
     result["data"] = "the reference's lame_test corpus WAVs (tests/golden/lame_test), encoded as one batch"
     result["job_latency_ms"] = None if lat is None else round(lat, 1)
     result["realtime_x"] = round(value / (44100 / 1e6), 2)

@@ -217,7 +217,9 @@ def encode_many(wavs, argv: Sequence[str] = (), rank: int = 0, world_size: int =
     """Encode a batch of WAVs (the C4 corpus case) as one job: every frame of
     every file in one launch per stage, the batch's frame list sharded across
     ranks by chunk count.  Returns one .gsc per file on rank 0
-    (None on the others; world_size > 1 needs torch.distributed initialised)."""
+    (None on the others; world_size > 1 needs torch.distributed initialised).
+    With a process group initialised the bytes always go through the
+    collective gather, also for one rank (`device`: where its tensors live)."""
     from .shard import frame_range_weighted, gather_files
 
     wavs = list(wavs)
@@ -227,7 +229,9 @@ def encode_many(wavs, argv: Sequence[str] = (), rank: int = 0, world_size: int =
         blob, sizes = p.encode_files(b, e)
     finally:
         p.close()
-    if world_size > 1:
+    import torch.distributed as dist
+
+    if world_size > 1 or (dist.is_available() and dist.is_initialized()):
         return gather_files(blob, sizes, device=device)
     outs, o = [], 0
     for n in sizes:

@@ -71,18 +71,24 @@ def broadcast_bounds(starts, ends, group=None, device=None, src: int = 0):
     return b[: len(b) // 2], b[len(b) // 2:]
 
 
+def free_port() -> int:
+    """A free TCP port on 127.0.0.1 for a rendezvous."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def spawn_workers(n: int, cmd: Sequence[str], env_extra: dict | None = None) -> int:
     """Launch `cmd` as n worker processes (RANK / LOCAL_RANK / WORLD_SIZE,
     rendezvous at 127.0.0.1 on a free port) and wait; the first non-zero exit
     ends the others.  Used by bench.py --gpus N before any GPU call."""
     import os
-    import socket
     import subprocess
     import time
 
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    port = free_port()
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),

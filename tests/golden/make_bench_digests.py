@@ -14,7 +14,7 @@ Keys (default: all, in this order): c2 at 1024 s (every frame); the
 weak-scaling c2 files of 2 / 4 / 8 ranks (1024 s per rank: every frame of the
 2-rank file, the first and last frame of every rank's range of the others);
 C5 at 3600 s, -cs8 and -cs4 (every frame: the whole 1-hour file); c2 at 600 s
-(every frame) and 3600 s (frames [0, 64));
+(every frame) and 3600 s (every frame);
 br128 and c3 at 1024 s (every frame); c2 at 16 s and 32 s (every frame: the
 GPU tests run bench.py on them).  Resumable: finished frames are kept.
 """
@@ -54,7 +54,7 @@ WORKLOADS = {
     "c5cs4:3600": ("c5cs4", 3600.0, "all"),
     # SURVEY.md §8d's C2 throughput lengths (600 s = 150 frames, 3600 s = 900)
     "c2:600": ("c2", 600.0, "all"),
-    "c2:3600": ("c2", 3600.0, ("range", 0, 64)),
+    "c2:3600": ("c2", 3600.0, "all"),
     "br128:1024": ("br128", 1024.0, "all"),
     "c3:1024": ("c3", 1024.0, "all"),
     # short files for the tests (bench.py --seconds 16, and 2 ranks x 16 s weak)
