@@ -59,6 +59,7 @@ struct ReduceFrame {
     uint64_t ystamps[16]; // out (GSC_STAMPS builds only): yakmo phase cycles (gsc_yakmo.hip)
     uint64_t acounts[64]; // out (GSC_STAMPS builds only): per wave, A1 queries home / pruned / evaluated, iterations, fixups, pending size
     uint64_t xcounts[16]; // out (GSC_STAMPS builds only, wave 0): iteration kinds and their cycles (gsc_scan.hip)
+    uint64_t xcounts2[16]; // out (GSC_STAMPS builds only, wave 0): solo resolutions against the speculative answer
 };
 
 // One frame of the encoder's per-frame DSP: FindAttenuationDivider

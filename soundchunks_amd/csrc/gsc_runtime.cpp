@@ -1845,6 +1845,14 @@ int gsc_scan_reduce(int n, int d0, const float* x, int k, float* centroids, int*
         std::fprintf(stderr, "\nfailed queries by cause: snapshot uncertified %llu, c* moved past m2 %llu, V check %llu"
                      " (V check only %llu)", (unsigned long long)x[12], (unsigned long long)x[13],
                      (unsigned long long)x[14], (unsigned long long)x[15]);
+        const uint64_t* x2 = fr[0].xcounts2;
+        std::fprintf(stderr, "\nsolo answer = speculative c*: by cause uncertified %llu, m2 %llu, V %llu | solos with a remainder"
+                             " %llu, of them same answer %llu (remainder queries valid to the next failure %llu, whole"
+                             " remainder valid %llu)", (unsigned long long)x2[0], (unsigned long long)x2[1],
+                     (unsigned long long)x2[2], (unsigned long long)x2[3], (unsigned long long)x2[4],
+                     (unsigned long long)x2[5], (unsigned long long)x2[6]);
+        std::fprintf(stderr, "\nin-batch DFS answers %llu, of them failing at commit %llu", (unsigned long long)x2[8],
+                     (unsigned long long)x2[9]);
         std::fprintf(stderr, "\n");
     }
     return 0;

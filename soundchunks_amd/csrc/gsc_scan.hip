@@ -60,6 +60,9 @@ namespace gsc {
 #ifndef GSC_DFS_CALL_D
 #define GSC_DFS_CALL_D 8  // feature widths whose exact DFS is an out-of-line call (A/B switch)
 #endif
+#ifndef GSC_INBATCH_DFS_D
+#define GSC_INBATCH_DFS_D 16  // widest D whose uncertified batch queries run the in-batch DFS (D = 32: +0.8 % C3 scan, its split-layout exact distances read the tail rows)
+#endif
 #ifndef GSC_EPSF8
 #define GSC_EPSF8 0x1p-18f  // A1 bound slack at D = 8 (< 56u of its 64u, see a1_dist_x2)
 #endif
@@ -154,9 +157,13 @@ __device__ __forceinline__ uint32_t rec_sib(const WaveRecT<SL>& r, int ls, int i
     return kInfBits;  // no slot levels below SL
 }
 
+// improvements of ANN's DFS kept per query for the in-batch DFS answers (valid
+// == 2 below): a DFS with more keeps its query uncertified (solo resolution)
+constexpr int kMaxImp = 8;
+
 template <int D>
 struct QRecT {        // A2 output per query
-    int valid;
+    int valid;        // 1: certified (A2), 2: ANN's answer on the snapshot by the exact DFS, 0: neither
     int cstar;        // kd-leaf position of the certified answer
     int id;           // centroid id (pidx[cstar])
     float g;          // snapshot distance to c*
@@ -164,8 +171,11 @@ struct QRecT {        // A2 output per query
     float rate;       // Single(1/sqrt(previous-pass count of c*))
     uint32_t farmask; // far steps on c*'s root path, bit = depth
     int pad_;         // 1: NaN-first query (ANN answers the NaN leaf its descent reaches)
-    float B[16];      // suffix max of box' over far steps (certificate thresholds)
+    float B[16];      // suffix max of box' over far steps (certificate thresholds);
+                      // valid == 2 (DFS answer): B[i] = the i-th improvement's distance
     float o[D];       // c*'s snapshot coordinates
+    int nimp;         // valid == 2: improvements of the snapshot DFS (the last one is c*)
+    int ir[kMaxImp];  // valid == 2: improvement i as DFS rank << 12 | kd-leaf position
 };
 
 template <class C>
@@ -972,7 +982,7 @@ __device__ __forceinline__ void vp_end(Scan2Shared<C>& sh, int qb, int off, int 
             sh.newc[par][j][C::ROW - 1] = nrm;
             sh.gp[j] = gpj;
 #ifdef GSC_STAMPS
-            if (!okc) sh.inval[j] = R.valid == 0 ? 1 : 2;  // cause (stamps): uncertified snapshot / c* moved past m2
+            if (!okc) sh.inval[j] = R.valid == 0 ? 1 : (R.valid == 2 ? 8 : 2);  // cause (stamps): uncertified / c* moved past m2 (DFS answer: away)
 #else
             if (!okc) sh.inval[j] = 1;
 #endif
@@ -980,6 +990,31 @@ __device__ __forceinline__ void vp_end(Scan2Shared<C>& sh, int qb, int off, int 
         wave_lds_sync();  // this round's newc feed the next round's lanes
         done |= rm;
     }
+}
+
+// A centroid at kd-leaf vp, moved since the snapshot to live distance du, and
+// the snapshot DFS answer of R (valid == 2; g = c*'s live distance): ANN's
+// improvement sequence -- and so its answer -- is unchanged when du is not
+// below the best-so-far at vp's DFS rank (ann_search inserts only strictly
+// smaller distances), vp was not an improvement itself, and c* did not move
+// away (vp_end).  The best-so-far at vp's rank is the distance of the last
+// improvement that ranks before vp; vp ranks after leaf p iff p's root path
+// takes the near child at the split where the two paths part, i.e. p's rank
+// (whose bit LOGK-1-l is the far step at depth l) has a 0 there.  Leaves the
+// DFS prunes need no case of their own: a leaf that is no improvement when
+// reached changes nothing whether or not it is reached.
+template <int LOGK, int D>
+__device__ __forceinline__ bool dfs_keeps(const QRecT<D>& R, float du, int vp, float g) {
+    const int n = R.nimp;
+#pragma unroll 1
+    for (int i = n - 1; i >= 0; --i) {
+        const int x = R.ir[i];
+        const int pos = x & 4095, rk = x >> 12;
+        if (vp == pos) return false;  // an earlier improvement moved (vp is never c* here)
+        const int l = __clz((uint32_t)(vp ^ pos)) - (32 - LOGK);
+        if (((rk >> (LOGK - 1 - l)) & 1) == 0) return !(du < (i == n - 1 ? g : R.B[i]));
+    }
+    return false;  // vp ranks before the first leaf reached: impossible (rank 0), kept conservative
 }
 
 // The same checks as work items taken by whichever wave is free (one-CU
@@ -1003,6 +1038,7 @@ __device__ __forceinline__ void v_check_grab(Scan2Shared<C>& sh, int qb, int off
     const int jr = j < pn ? j : 0;
     const QRecT<D>& R = sh.qrec[qb][off + jr];
     const bool act = j < pn && R.pad_ == 0;  // a NaN-first answer holds whatever moved
+    const bool dfsa = R.valid == 2;          // the snapshot DFS answer (dfs_keeps)
     const int cs = R.cstar;
     const uint32_t fm = R.farmask;
     const float g = sh.gp[jr];
@@ -1036,8 +1072,13 @@ __device__ __forceinline__ void v_check_grab(Scan2Shared<C>& sh, int qb, int off
                 du1 = fadd(du1, fmul(t1, t1));
             }
             const bool far0 = (fm >> (lca0 & 31)) & 1u, far1 = (fm >> (lca1 & 31)) & 1u;
-            if (u0 && !(du0 > g && (!far0 || du0 > b0))) bad = true;
-            if (u1 && !(du1 > g && (!far1 || du1 > b1))) bad = true;
+            if (!dfsa) {
+                if (u0 && !(du0 > g && (!far0 || du0 > b0))) bad = true;
+                if (u1 && !(du1 > g && (!far1 || du1 > b1))) bad = true;
+            } else {
+                if (u0 && !dfs_keeps<LOGK, D>(R, du0, vp0, g)) bad = true;
+                if (u1 && !dfs_keeps<LOGK, D>(R, du1, vp1, g)) bad = true;
+            }
         }
         t = __builtin_amdgcn_readfirstlane(tn);
     }
@@ -1060,13 +1101,16 @@ __device__ __forceinline__ void v_check_grab(Scan2Shared<C>& sh, int qb, int off
 // their trees can have cells whose bounds contradict the cut values (NaN cuts
 // upstream), so box' can shrink along a path (negative increments) and the
 // innermost-far-subtree test is not enough; they run scan_exact_dfs.
+//
+// With `rec` the improvements (DFS rank, leaf, distance) go to rec->ir / B /
+// nimp (thread 0): the in-batch DFS answers' validity check (v_check_grab)
+// replays the rank order of a moved centroid against them.
 template <class C>
-__device__ __forceinline__ void dfs_parallel(Scan2Shared<C>& sh, int tid, int lane, int wave, int& out_pos,
-                                             float& out_key) {
+__device__ __forceinline__ void dfs_parallel(Scan2Shared<C>& sh, const float* __restrict__ q, int tid, int lane,
+                                             int wave, int& out_pos, float& out_key, QRecT<C::D>* rec = nullptr) {
     constexpr int D = C::D, LOGK = C::LOGK, NW = C::NWL;
     constexpr int K = 1 << LOGK;
     constexpr int nthreads = 64 * NW;
-    const float* q = sh.qslow;
     for (int h = tid; h < K - 1; h += nthreads) {  // split nodes: box' increment, sign = near child hi
         const int cdim = sh.t.cd[h];
         const float qc = q[cdim];
@@ -1130,7 +1174,7 @@ __device__ __forceinline__ void dfs_parallel(Scan2Shared<C>& sh, int tid, int la
         }
     }
     // improvements: the empty list takes the first leaf reached (max_key = FLT_MAX)
-    int pos = -1, bp = -1, par = 0;
+    int pos = -1, bp = -1, par = 0, nimp = 0;
     float b = FLT_MAX;
     for (;;) {
         uint32_t key = 0xFFFFFFFFu;
@@ -1157,7 +1201,13 @@ __device__ __forceinline__ void dfs_parallel(Scan2Shared<C>& sh, int tid, int la
         pos = (int)(g >> 12);
         bp = (int)(g & 4095u);
         b = sh.dist[bp];
+        if (rec && tid == 0 && nimp < kMaxImp) {
+            rec->ir[nimp] = (int)g;
+            rec->B[nimp] = b;
+        }
+        ++nimp;
     }
+    if (rec && tid == 0) rec->nimp = nimp;
     out_pos = bp;
     out_key = b;
 }
@@ -1166,9 +1216,9 @@ __device__ __forceinline__ void dfs_parallel(Scan2Shared<C>& sh, int tid, int la
 // kernel 20 spilled VGPRs elsewhere and the call costs nothing measurable
 // (C5 -cs4 6336 vs 6335 ms); at D = 16 the inlined DFS is 0.4 % faster
 template <class C>
-__device__ __noinline__ void dfs_parallel_call(Scan2Shared<C>& sh, int tid, int lane, int wave, int& out_pos,
-                                               float& out_key) {
-    dfs_parallel<C>(sh, tid, lane, wave, out_pos, out_key);
+__device__ __noinline__ void dfs_parallel_call(Scan2Shared<C>& sh, const float* __restrict__ q, int tid, int lane,
+                                               int wave, int& out_pos, float& out_key, QRecT<C::D>* rec) {
+    dfs_parallel<C>(sh, q, tid, lane, wave, out_pos, out_key, rec);
 }
 
 // Exact ANN search of the NaN passes, all threads.  NaN cut values and the
@@ -1187,12 +1237,11 @@ __device__ __noinline__ void dfs_parallel_call(Scan2Shared<C>& sh, int tid, int 
 // and dead leaves carry +inf in sh.dist and never improve.  Same answers as
 // ANN's sequential walk (annkSearch @0x1800124b0; the oracle's ann_oracle.c).
 template <class C>
-__device__ __noinline__ void dfs_parallel_nan(Scan2Shared<C>& sh, int tid, int lane, int wave, int& out_pos,
-                                                 float& out_key) {
+__device__ __noinline__ void dfs_parallel_nan(Scan2Shared<C>& sh, const float* __restrict__ q, int tid, int lane,
+                                                 int wave, int& out_pos, float& out_key, QRecT<C::D>* rec) {
     constexpr int D = C::D, LOGK = C::LOGK, NW = C::NWL;
     constexpr int K = 1 << LOGK;
     constexpr int nthreads = 64 * NW;
-    const float* q = sh.qslow;
     for (int h0 = 0; h0 < K; h0 += nthreads) {  // split nodes: signed box' increment, near child
         const int h = h0 + tid;
         bool nearlo = false;
@@ -1277,7 +1326,7 @@ __device__ __noinline__ void dfs_parallel_nan(Scan2Shared<C>& sh, int tid, int l
         sb[s8][1] = fmaxf(fb[1], fb[2]);
         sb[s8][0] = fmaxf(fb[0], sb[s8][1]);
     }
-    int pos = -1, bp = -1, par = 0;
+    int pos = -1, bp = -1, par = 0, nimp = 0;
     float b = FLT_MAX;  // the empty list's max_key
     for (;;) {
         uint32_t key = 0xFFFFFFFFu;
@@ -1322,7 +1371,13 @@ __device__ __noinline__ void dfs_parallel_nan(Scan2Shared<C>& sh, int tid, int l
         pos = (int)(g >> 12);
         bp = (int)(g & 4095u);
         b = sh.dist[bp];
+        if (rec && tid == 0 && nimp < kMaxImp) {  // the improvement sequence (as dfs_parallel)
+            rec->ir[nimp] = (int)g;
+            rec->B[nimp] = b;
+        }
+        ++nimp;
     }
+    if (rec && tid == 0) rec->nimp = nimp;
     out_pos = bp;
     out_key = b;
 }
@@ -1523,6 +1578,9 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     constexpr int D = C::D, K = C::K, SL = C::SL, LS = C::LS, NWL = C::NWL, KB = C::KB;
     constexpr int kErrWave = NWL > 1 ? 1 : 0;  // residual + cluster ids (wave 0 keeps the log)
     constexpr bool PRUNE = true;               // A1 pruning by wave boxes
+    // uncertified queries of a batch resolved in the batch by the exact DFS on the
+    // snapshot (see the fixups below); GSC_INBATCH_DFS_D: the widest D that does it
+    constexpr bool kInBatchDfs = D <= GSC_INBATCH_DFS_D;
     const bool no_half = (opts & 1) != 0;      // diagnostic: full-dimension A1 bounds in every pass
     const bool no_prune = (opts & 2) != 0;     // experiment: every wave evaluates every query (no mid-A1 barrier)
     // experiment (opts bits 8..15): queries per speculative batch below KB
@@ -1780,6 +1838,11 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     int lg_pos = -1, lg_tag = 0;
     double err = 0.0;
     int slow_total = 0, restarts = 0;
+    // in-batch DFS answers of this pass, and how many failed at the commit: on
+    // frames whose answers rarely survive (quiet audio among NaN centroids:
+    // 2 in 3 fail on the corpus' 60.wav) the DFS would be paid twice, so the
+    // pass stops using it once a third of them fail (uniform counters)
+    int ib_try = 0, ib_fail = 0;
     bool guard = false;  // the progress guard tripped
 #ifdef GSC_STAMPS
     uint64_t acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1787,6 +1850,9 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     // wave 0: bubble iterations / cycles, other iterations / cycles, iterations with fixups / cycles,
     // iterations with a solo resolution / cycles, new queries, A2 queries needing per-wave bounds
     uint64_t xc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // solo resolutions: same answer as the speculative c* by cause (uncertified / m2 / V), with a
+    // remainder, same answer with a remainder, remainder queries valid up to the next failure, whole remainder valid
+    uint64_t xc2[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tlast = stamp();
     acc[9] = tlast - t_kernel0;  // pass setup: tree build, registers, first queries
 #endif
@@ -1797,6 +1863,36 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
     int vq_buf1 = 0, vq_s1 = 0, vq_off1 = 0, vq_n1 = 0, vq_a11 = 0;
     int nvq = 0;
     int cur_buf = 0, cur_s = 0, cur_n = n0;  // batch whose distances are computed this iteration
+    // every leaf's exact distance to q (ANN's sequential sum) into sh.dist, from
+    // the registers as they are (+inf for slots without a live centroid)
+    auto exact_dists = [&](const float* __restrict__ qe) {
+        float dv[SL];
+#pragma unroll
+        for (int s = 0; s < SL; ++s) dv[s] = 0.0f;
+#pragma unroll
+        for (int d = 0; d < C::DR; ++d) {
+            const float qd = qe[d];
+#pragma unroll
+            for (int s = 0; s < SL; ++s) {
+                const float t = fsub(qd, creg[s][d]);
+                dv[s] = fadd(dv[s], fmul(t, t));
+            }
+        }
+        if constexpr (C::SPLIT) {  // every leaf's full distance: the tail rows (rare path)
+#pragma unroll
+            for (int s = 0; s < SL; ++s) {
+                const float* tr = trow + (int64_t)(p0 + s) * C::TL;
+                if (!((dmask >> s) & 1u))
+                    for (int d = 0; d < C::TL; ++d) {
+                        const float t = fsub(qe[C::DR + d], tr[d]);
+                        dv[s] = fadd(dv[s], fmul(t, t));
+                    }
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < SL; ++s)
+            if (p0 + s < K) sh.dist[p0 + s] = ((dmask >> s) & 1u) ? __builtin_inff() : dv[s];
+    };
     int next_load = n0;
     for (int it = 0;; ++it) {
         int ln = opaque_v(lane);  // see opaque_v: refreshed per phase below
@@ -1952,9 +2048,13 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             fj = bad ? __ffsll((long long)bad) - 1 : -1;
         }
         const int kc = has_p ? (fj >= 0 ? fj : P_n) : 0;  // committed prefix of the pending batch
+        if (kInBatchDfs && fj >= 0) ib_fail += uniform_int(sh.qrec[P_buf][P_off + fj].valid) == 2 ? 1 : 0;
 #ifdef GSC_STAMPS
+        int fj_cause = 0;
         if (fj >= 0) {  // why the first failing query failed
             const int cause = sh.inval[fj];
+            fj_cause = cause;
+            xc2[9] += sh.qrec[P_buf][P_off + fj].valid == 2 ? 1 : 0;  // a DFS answer failed its check
             xc[12] += (cause & 1) ? 1 : 0;
             xc[13] += (cause & 2) ? 1 : 0;
             xc[14] += (cause & 4) ? 1 : 0;
@@ -2066,6 +2166,66 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 for (int j0 = wave * 4; j0 < nfx; j0 += 4 * NWL)
                     a2_group<C, false>(sh, j0, nfx, sh.q[A_buf], sh.qrec[A_buf], 0, sh.fxl, ln);
                 lds_barrier();
+                // Queries the exact certificate cannot decide either: ANN's stale-tree
+                // DFS does not provably reach the snapshot's minimum (and mostly does
+                // not: 96 % of them resolve elsewhere), or an exact tie.  Their
+                // answer on the snapshot is ANN's search itself -- the exact DFS over
+                // the snapshot registers (they change only at the fold below) -- and
+                // the commit checks it like a certificate: a centroid moved since
+                // the snapshot keeps the DFS's improvement sequence when its live
+                // distance is not below the best-so-far at its DFS rank
+                // (v_check_grab), c* itself when it did not move away (vp_end).
+                // Without this such a query fails its commit, is resolved alone and
+                // holds the next batch back for an iteration.
+                if (kInBatchDfs && 3 * ib_fail <= ib_try + 8) {
+                    uint64_t ux = __ballot(((fx >> ln) & 1ull) && sh.qrec[A_buf][ln].valid == 0);
+                    const bool any_ux = ux != 0;
+                    ib_try += __popcll(ux);
+#pragma unroll 1
+                    while (ux) {
+                        const int jj = __ffsll((long long)ux) - 1;
+                        ux &= ux - 1;
+                        QRecT<D>& R = sh.qrec[A_buf][jj];
+                        exact_dists(sh.q[A_buf][jj]);
+                        lds_barrier();  // sh.dist complete
+                        int bpos;
+                        float key;
+                        // NaN passes: NaN and dead leaves are +inf in sh.dist, inert as in the
+                        // solo resolution; NaN-first queries are certified (a2_group)
+                        if (nan_rows)
+                            dfs_parallel_nan<C>(sh, sh.q[A_buf][jj], tid, ln, wave, bpos, key, &R);
+                        else
+                            dfs_parallel_call<C>(sh, sh.q[A_buf][jj], tid, ln, wave, bpos, key, &R);
+                        bpos = uniform_int(bpos);
+                        // c*'s snapshot coordinates from its owner; the record from thread 0
+                        const int owner_t = bpos >> LS, slot = bpos & (SL - 1);
+#pragma unroll
+                        for (int s = 0; s < SL; ++s)
+                            if (s == slot && tid == owner_t) {
+#pragma unroll
+                                for (int d = 0; d < C::DR; ++d) R.o[d] = creg[s][d];
+                                if constexpr (C::SPLIT)
+                                    for (int d = C::DR; d < D; ++d) R.o[d] = trow[(int64_t)bpos * C::TL + (d - C::DR)];
+                            }
+                        if (tid == 0) {
+                            R.cstar = bpos;
+                            R.id = sh.t.pidx[bpos];
+                            R.g = key;
+                            // vp_end's "c* moved: live d < m2" becomes d <= key: a c* that
+                            // moved closer stays the DFS's last improvement, and every leaf
+                            // after it was at or above key
+                            R.m2 = __uint_as_float(__float_as_uint(key) + 1u);
+                            R.rate = sh.rate[bpos];
+                            R.valid = (R.nimp <= kMaxImp && key <= FLT_MAX) ? 2 : 0;
+                        }
+#ifdef GSC_STAMPS
+                        xc2[8] += 1;
+#endif
+                    }
+                    // the records are complete (the commit's update chain reads R.o next iteration,
+                    // at D = 8 before any other barrier)
+                    if (any_ux) lds_barrier();
+                }
             }
         }
         // every wave folds the committed updates of the centroids it owns, straight
@@ -2128,7 +2288,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
             // gives ANN's answer whether or not a new certificate would pass
             // (41 % of the restarts on the C2 frame; the fresh A1 + A2 they skip
             // cost about 10k cycles each)
-            const bool snap_failed = uniform_int(sh.qrec[P_buf][P_off + fj].valid) == 0;
+            const bool snap_failed = uniform_int(sh.qrec[P_buf][P_off + fj].valid) != 1;
             if (!snap_failed) {
                 a1_query<C>(creg, sh.qslow, sh.wrec[vwave][KB], vwave, ln, dmask, trow, p0, tw_pass);
                 lds_barrier();
@@ -2144,48 +2304,40 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
                 bpos = uniform_int(sh.qsolo.cstar);
                 key = sh.qsolo.g;
             } else {
-                float dv[SL];
-#pragma unroll
-                for (int s = 0; s < SL; ++s) dv[s] = 0.0f;
-#pragma unroll
-                for (int d = 0; d < C::DR; ++d) {
-                    const float qd = sh.qslow[d];
-#pragma unroll
-                    for (int s = 0; s < SL; ++s) {
-                        const float t = fsub(qd, creg[s][d]);
-                        dv[s] = fadd(dv[s], fmul(t, t));
-                    }
-                }
-                if constexpr (C::SPLIT) {  // every leaf's full live distance: the tail rows (rare path)
-#pragma unroll
-                    for (int s = 0; s < SL; ++s) {
-                        const float* tr = trow + (int64_t)(p0 + s) * C::TL;
-                        if (!((dmask >> s) & 1u))
-                            for (int d = 0; d < C::TL; ++d) {
-                                const float t = fsub(sh.qslow[C::DR + d], tr[d]);
-                                dv[s] = fadd(dv[s], fmul(t, t));
-                            }
-                    }
-                }
-#pragma unroll
-                for (int s = 0; s < SL; ++s)
-                    if (p0 + s < K) sh.dist[p0 + s] = ((dmask >> s) & 1u) ? __builtin_inff() : dv[s];
+                exact_dists(sh.qslow);
                 // the centroid registers stay live across the DFS (it needs ~40 more
                 // VGPRs; parking the 128 in C and reloading them cost 2x the DFS time)
                 lds_barrier();  // sh.dist complete
                 if (nan_rows) {
                     // NaN leaves carry +inf here: inert, as the query's descent
                     // reaches a real leaf first (NaN-first queries never fail)
-                    dfs_parallel_nan<C>(sh, tid, ln, wave, bpos, key);
+                    dfs_parallel_nan<C>(sh, sh.qslow, tid, ln, wave, bpos, key, nullptr);
                 } else if constexpr (D <= GSC_DFS_CALL_D) {
-                    dfs_parallel_call<C>(sh, tid, ln, wave, bpos, key);
+                    dfs_parallel_call<C>(sh, sh.qslow, tid, ln, wave, bpos, key, nullptr);
                 } else {
-                    dfs_parallel<C>(sh, tid, ln, wave, bpos, key);
+                    dfs_parallel<C>(sh, sh.qslow, tid, ln, wave, bpos, key);
                 }
                 bpos = uniform_int(bpos);
                 ++slow_total;
                 STAMP(11)
             }
+#ifdef GSC_STAMPS
+            {
+                const bool same = bpos == sh.vcs[fj];
+                const bool rem = fj + 1 < P_n;
+                const uint64_t badm = __ballot(ln > fj && ln < P_n && sh.inval[ln] != 0);
+                const int nb = badm ? __ffsll((long long)badm) - 1 : P_n;
+                if (same) {
+                    xc2[(fj_cause & 1) ? 0 : ((fj_cause & 2) ? 1 : 2)] += 1;
+                    if (rem) {
+                        xc2[4] += 1;
+                        xc2[5] += (uint64_t)(nb - fj - 1);
+                        xc2[6] += nb == P_n ? 1 : 0;
+                    }
+                }
+                xc2[3] += rem ? 1 : 0;
+            }
+#endif
             // owner publishes c's coordinates; tid 0 moves it (encoder.lpr:735-744);
             // the move enters the log (later batches' snapshots miss it) and the registers
             const int owner_t = bpos >> LS, slot = bpos & (SL - 1);  // owner thread
@@ -2277,6 +2429,8 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         for (int k = 0; k < 8; ++k) frp->acounts[wave * 8 + k] += acn[k];
     if (tid == 0)
         for (int k = 0; k < 16; ++k) frp->xcounts[k] += xc[k];
+    if (tid == 0)
+        for (int k = 0; k < 16; ++k) frp->xcounts2[k] += xc2[k];
 #endif
     const double diff = err > prev_err ? err - prev_err : prev_err - err;
     const bool done = diff <= tol || pass + 1 >= kMaxScanIters || guard;
