@@ -460,12 +460,13 @@ def base_result(args, ws, dt, value, desc, enc, tm, cs, argv, rate, ch) -> dict:
                     None)
         if kern and K == 4096:
             traffic = kern["hbm_bytes_per_frame_per_launch"] * tm["reduce_frames"]
-    # measured VALU issue fraction of the scan kernel (SQ pass of the same build:
-    # VALU wave-instructions x 2 cycles / (4 SIMDs x CUs x launch cycles)), next to
-    # the algorithm-equivalent frac above -- D = 16 (the C2 shape) only
-    issue = None
-    if SQ_SUMMARY.exists() and cs == 8 and K == 4096:
-        issue = json.loads(SQ_SUMMARY.read_text()).get("scan_valu_issue_frac")
+    # VALU issue fraction of the scan kernel from the committed SQ pass (VALU
+    # wave-instructions x 2 cycles / (4 SIMDs x CUs x launch cycles)) -- a profile
+    # of the C2 shape, so it is attached to the C2 line only, with its source
+    issue = sq = None
+    if SQ_SUMMARY.exists() and args.config == "c2":
+        sq = json.loads(SQ_SUMMARY.read_text())
+        issue = sq.get("scan_valu_issue_frac")
     metric = "encoded Msamples/s @44.1kHz stereo ChunkSize=8 ChunkCount=4096; bit-exact .gsc"  # BASELINE.json
     if args.config != "c2":
         metric = f"encoded Msamples/s ({desc}); bit-exact .gsc"
@@ -492,10 +493,12 @@ def base_result(args, ws, dt, value, desc, enc, tm, cs, argv, rate, ch) -> dict:
                      "hbm_frac": None if traffic is None or avg_launch_s <= 0 else
                      round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 6),
                      "avg_launch_ms": round(avg_launch_s * 1e3, 3), "ops_per_launch": ops / launches,
-                     "valu_issue_frac": None if issue is None else round(issue, 4),
-                     "valu_issue_note": "measured: SQ_INSTS_VALU x 2 cycles / (4 SIMDs x frames x launch cycles at "
-                                        "2.4 GHz), profiles/r05/pmc_sq_summary.json (C2 shape); frac counts the "
-                                        "reference's brute-force ops, which the kernel does not execute"},
+                     "profiled_c2_valu_issue_frac": None if issue is None else round(issue, 4),
+                     "valu_issue_note": None if issue is None else
+                     f"from the committed SQ pass {SQ_SUMMARY.relative_to(ROOT)} (C2 shape, build "
+                     f"{sq.get('source_commit', 'unrecorded')}), not this run: SQ_INSTS_VALU x 2 cycles / (4 SIMDs x "
+                     f"frames x launch cycles at 2.4 GHz); frac above counts the reference's brute-force ops, which "
+                     f"the kernel does not execute"},
         # host_post_ms: what the KNNFit / prune / packing pipeline adds after the
         # scan; post_overlap_ms: the part of it that ran in the scan tail
         "stages_ms": {k: round(tm[k], 1) for k in ("host_frames_ms", "gpu_dsp_ms", "gpu_yakmo_ms", "gpu_scan_ms",

@@ -4,7 +4,7 @@
 # then the in-tree stamps library on one C2 and one -cs4 frame
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 170 --timeout-method thread \
   -k "${PTESTS:-scan or gsc_matches_golden or corpus_as_one_batch or bench or overflow}" > gpurun_out/ab_test.log 2>&1
 rc=$?; tail -2 gpurun_out/ab_test.log; [ $rc -ne 0 ] && exit $rc
 lib() { [ "$1" = tree ] && echo soundchunks_amd/lib/libsoundchunks_amd.so || echo soundchunks_amd/lib/variants/$1/libsoundchunks_amd.so; }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5: the full -m gpu suite, smoke(), then the default C2 bench (1024 s) without the CPU leg
+# the full -m gpu suite, smoke(), then the default C2 bench (1024 s) without the CPU leg
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/suite.log 2>&1
