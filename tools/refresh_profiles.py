@@ -21,8 +21,18 @@ def short(n):
     return re.sub(r"\(.*$", "", n)
 
 
+def head_commit() -> str:
+    """The commit the profiled build came from (+ "-dirty" with uncommitted source changes)."""
+    h = subprocess.run(["git", "-C", str(ROOT), "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                       text=True).stdout.strip()
+    dirty = subprocess.run(["git", "-C", str(ROOT), "status", "--porcelain", "--", "soundchunks_amd", "bench.py"],
+                           capture_output=True, text=True).stdout.strip()
+    return h + ("-dirty" if dirty else "")
+
+
 def main(rnd):
     out = ROOT / "profiles" / rnd
+    commit = head_commit()
     out.mkdir(parents=True, exist_ok=True)
     stats = subprocess.run([sys.executable, str(ROOT / "tools/rocpd_summary.py"), str(PROF / "trace/run_results.db")],
                            check=True, capture_output=True, text=True).stdout
@@ -46,7 +56,7 @@ def main(rnd):
                            "bench.py --seconds 256 --steps 1 --warmup 0 (64 frames)"],
                           check=True, capture_output=True, text=True).stdout
     (out / "pmc_summary.json").write_text(summ)
-    if (PROF / "sq" / "run_results.db").exists():  # the SQ pass (tools/gpu/profile_r05.sh)
+    if (PROF / "sq" / "run_results.db").exists():  # the SQ pass (tools/gpu/profile.sh)
         sql = [l for l in (PROF / "sq.log").read_text().splitlines() if l.startswith("{")][-1]
         sqj = json.loads(sql)
         summ = subprocess.run([sys.executable, str(ROOT / "tools/sq_summary.py"), str(PROF / "sq/run_results.db"),
@@ -54,11 +64,13 @@ def main(rnd):
                                "rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS "
                                "SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_WAIT_ANY -- python3 bench.py --seconds 64 --steps 1 "
                                f"--warmup 0 --no-cpu-baseline ({sqj['config']['frames']} C2 frames, MI355X, "
-                               "tools/gpu/profile_r05.sh)"], check=True, capture_output=True, text=True).stdout
+                               "tools/gpu/profile.sh)", commit], check=True, capture_output=True, text=True).stdout
         (out / "pmc_sq_summary.json").write_text(summ)
     if (PROF / "bench_default.log").exists():
         line = [l for l in (PROF / "bench_default.log").read_text().splitlines() if l.startswith("{")][-1]
-        (out / "bench_1gpu.json").write_text(line + "\n")
+        d = json.loads(line)
+        d["source_commit"] = commit  # recorded here: the GPU box's snapshot has no .git
+        (out / "bench_1gpu.json").write_text(json.dumps(d) + "\n")
         print(json.loads(line)["value"])
 
 

@@ -2,7 +2,7 @@
 counters (SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS
 SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_WAIT_ANY) over a short C2 bench:
 
-    python tools/sq_summary.py SQ.db FRAMES SEARCHES "source" > profiles/r05/pmc_sq_summary.json
+    python tools/sq_summary.py SQ.db FRAMES SEARCHES "source" [commit] > profiles/rNN/pmc_sq_summary.json
 
 Per kernel: the counter sums and the summed dispatch duration.  For the scan
 kernel: instructions per search and the measured VALU issue fraction = VALU
@@ -25,7 +25,7 @@ def short(n):
     return re.sub(r"\(.*$", "", n)
 
 
-def main(db, frames, searches, source):
+def main(db, frames, searches, source, commit=None):
     frames, searches = int(frames), int(searches)
     c = sqlite3.connect(db)
     acc = defaultdict(lambda: defaultdict(float))
@@ -35,7 +35,7 @@ def main(db, frames, searches, source):
         k = short(name)
         acc[k][ctr] += float(val)
         dur[k][disp] = (e - s) * 1e-9
-    out = {"source": source, "units": "SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_BUSY_CYCLES as reported (quad-cycles); "
+    out = {"source": source, "source_commit": commit, "units": "SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_BUSY_CYCLES as reported (quad-cycles); "
                                       "instruction counts summed over waves; duration_s = summed dispatch durations",
            "kernels": {}}
     for k in sorted(acc):
@@ -56,4 +56,4 @@ def main(db, frames, searches, source):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    main(*sys.argv[1:6])
