@@ -171,6 +171,12 @@ int gsc_scan_reduce(int n, int d, const float *x, int k, float *centroids, int *
  * Single features of one frame -> labels[n] in [0, k). */
 int gsc_birch_labels(int n, int d, const float *x, int k, int *labels);
 int gsc_knnfit_assign(int r, int cs, const float *cand_fwd, int n, const float *q, float eps, int *best);
+/* yakmo's prefix-chain fast path (gsc_yakmo.hip chain_fast, ppl = 8 or 16
+ * points per lane) on 64*nbk points from *run: the accepted block count, the
+ * run after them, and per accepted block the checkpoint / min / max of the
+ * running f32 total (the DLL's sequential cum[], App. C.1).  Parity tests. */
+int gsc_yakmo_chain_test(int ppl, const float *pts, int nbk, float run, int *accepted, float *run_out, float *ck,
+                         float *bmn, float *bmx);
 
 /* Timing of the last gsc_encode_* call on the calling thread (milliseconds),
  * split per stage, plus average device time per launch of each kernel. */

@@ -113,6 +113,8 @@ SIGNATURES = {
     "gsc_frame_dsp": (ctypes.c_int, [_U8P, ctypes.c_size_t, ctypes.POINTER(GscOptions), ctypes.c_int, _IP,
                                      ctypes.POINTER(_FP), _IP]),
     "gsc_yakmo_seed_means": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _FP, ctypes.c_int, _FP]),
+    "gsc_yakmo_chain_test": (ctypes.c_int, [ctypes.c_int, _FP, ctypes.c_int, ctypes.c_float, _IP, _FP, _FP, _FP,
+                                            _FP]),
     "gsc_scan_reduce": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _FP, ctypes.c_int, _FP, _IP, ctypes.c_int, _IP]),
     "gsc_birch_labels": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _FP, ctypes.c_int, _IP]),
     "gsc_knnfit_assign": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _FP, ctypes.c_int, _FP, ctypes.c_float, _IP]),

@@ -1739,6 +1739,33 @@ static std::vector<float> pad_rows(const float* x, int n, int d, int dp) {
     return v;
 }
 
+extern "C" hipError_t gsc_launch_yakmo_chain_test(int ppl, const float* pts, int nbk, float run, int* k_out,
+                                                  float* out);
+
+int gsc_yakmo_chain_test(int ppl, const float* pts, int nbk, float run, int* accepted, float* run_out, float* ck,
+                         float* bmn, float* bmx) {
+    if (ensure_device() != 0) return -1;
+    if ((ppl != 8 && ppl != 16) || nbk < 1 || nbk > ppl) return fail("gsc_yakmo_chain_test: ppl 8 / 16, 1 <= nbk <= ppl");
+    DevBuf<float> dP, dO;
+    DevBuf<int> dK;
+    HIP_TRY(dP.alloc(size_t(64) * nbk));
+    HIP_TRY(dO.alloc(1 + 3 * 64));
+    HIP_TRY(dK.alloc(1));
+    HIP_TRY(hipMemcpy(dP.p, pts, sizeof(float) * 64 * size_t(nbk), hipMemcpyHostToDevice));
+    HIP_TRY(gsc_launch_yakmo_chain_test(ppl, dP.p, nbk, run, dK.p, dO.p));
+    HIP_TRY(hipDeviceSynchronize());
+    float o[1 + 3 * 64];
+    HIP_TRY(hipMemcpy(o, dO.p, sizeof(o), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(accepted, dK.p, sizeof(int), hipMemcpyDeviceToHost));
+    *run_out = o[0];
+    for (int b = 0; b < nbk; ++b) {
+        ck[b] = o[1 + b];
+        bmn[b] = o[1 + 64 + b];
+        bmx[b] = o[1 + 128 + b];
+    }
+    return 0;
+}
+
 int gsc_yakmo_seed_means(int n, int d0, const float* x, int k, float* centroids) {
     if (ensure_device() != 0) return -1;
     if (k >= n || k <= 0 || k > kMaxK) return fail("yakmo needs 0 < k < n, k <= 4096");

@@ -60,6 +60,9 @@ namespace gsc {
 #ifndef GSC_DFS_CALL_D
 #define GSC_DFS_CALL_D 8  // feature widths whose exact DFS is an out-of-line call (A/B switch)
 #endif
+#ifndef GSC_VP_EARLY_D
+#define GSC_VP_EARLY_D 8  // widest D whose update chain runs right after its prep (A/B switch, see kVpEarly)
+#endif
 #ifndef GSC_INBATCH_DFS_D
 #define GSC_INBATCH_DFS_D 16  // widest D whose uncertified batch queries run the in-batch DFS (D = 32: +0.8 % C3 scan, its split-layout exact distances read the tail rows)
 #endif
@@ -1913,7 +1916,7 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         // as soon as a wave is done with A1 (wave 0 reaches the mid-A1 barrier
         // early).  C5 -cs4 scan -3.2 % (5551 vs 5732 ms at 128 s) and no VGPR
         // spill left; at D = 16 +0.6 % (3361 vs 3342 ms), so it stays after A1
-        constexpr bool kVpEarly = D <= 8;
+        constexpr bool kVpEarly = D <= GSC_VP_EARLY_D;
         if constexpr (kVpEarly) {
             if (wave == 0 && has_p) {
                 vp_end<C>(sh, P_buf, P_off, P_n, ln, lg_pos, vst, half, it & 1);
@@ -2139,7 +2142,8 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         lds_barrier();
         if (A_n > 0) {
             // queries the approximate certificate could not decide: exact A1 + A2
-            // (on the registers as folded above)
+            // on the snapshot registers (fold_commits runs after the fixups: a
+            // pruned wave's lower bound holds for the snapshot only)
             const uint64_t fx = __ballot(ln < A_n && sh.qrec[A_buf][ln].valid == 0);
             if (fx) {
                 const int nfx = __popcll(fx);

@@ -784,9 +784,47 @@ __global__ __launch_bounds__(kYThreads) void yakmo_seed2_kernel(const ReduceFram
     }
 }
 
+// Test hook (tests/test_gpu_yakmo_chain.py): one wave runs chain_fast<PPL> on
+// a ring of nbk 64-point blocks starting at run, so that the integer prefix
+// path (ties, negative runs, zero runs, NaN / inf, binade crossings) is
+// checked point for point against the sequential f32 chain it replaces.
+template <int PPL>
+__global__ __launch_bounds__(64) void yakmo_chain_test_kernel(const float* __restrict__ pts, int nbk, float run,
+                                                              int* __restrict__ k_out, float* __restrict__ out) {
+    __shared__ alignas(16) float ring[64 * PPL];
+    __shared__ float ck[64], bmn[64], bmx[64];
+    const int lane = threadIdx.x;
+    for (int i = lane; i < 64 * PPL; i += 64) ring[i] = i < 64 * nbk ? pts[i] : 0.0f;
+    for (int i = lane; i < 64; i += 64) ck[i] = bmn[i] = bmx[i] = __builtin_nanf("");
+    __syncthreads();
+    float r = run;
+    const int k = chain_fast<PPL>(ring, 0, nbk, lane, &r, ck, bmn, bmx, 0);
+    __syncthreads();
+    if (lane == 0) {
+        *k_out = k;
+        out[0] = r;
+    }
+    if (lane < nbk) {
+        out[1 + lane] = ck[lane];
+        out[1 + 64 + lane] = bmn[lane];
+        out[1 + 128 + lane] = bmx[lane];
+    }
+}
+
 }  // namespace gsc
 
 using namespace gsc;
+
+// nbk <= 64 / (64 / PPL) blocks: out = run, then ck[64], bmn[64], bmx[64]
+extern "C" hipError_t gsc_launch_yakmo_chain_test(int ppl, const float* pts, int nbk, float run, int* k_out,
+                                                  float* out) {
+    if (nbk < 1 || nbk > ppl || (ppl != 8 && ppl != 16)) return hipErrorInvalidValue;
+    if (ppl == 8)
+        hipLaunchKernelGGL(yakmo_chain_test_kernel<8>, dim3(1), dim3(64), 0, nullptr, pts, nbk, run, k_out, out);
+    else
+        hipLaunchKernelGGL(yakmo_chain_test_kernel<16>, dim3(1), dim3(64), 0, nullptr, pts, nbk, run, k_out, out);
+    return hipGetLastError();
+}
 
 // gsum / gbits: HBM state of frames over kYMaxLds points (see yakmo_seed2_kernel;
 // gsc_yakmo_big_floats / _words give the sizes); unused otherwise
