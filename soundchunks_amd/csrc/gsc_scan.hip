@@ -61,7 +61,7 @@ namespace gsc {
 #define GSC_DFS_CALL_D 8  // feature widths whose exact DFS is an out-of-line call (A/B switch)
 #endif
 #ifndef GSC_VP_EARLY_D
-#define GSC_VP_EARLY_D 8  // widest D whose update chain runs right after its prep (A/B switch, see kVpEarly)
+#define GSC_VP_EARLY_D 32  // widest D whose update chain runs right after its prep (A/B switch, see kVpEarly)
 #endif
 #ifndef GSC_INBATCH_DFS_D
 #define GSC_INBATCH_DFS_D 16  // widest D whose uncertified batch queries run the in-batch DFS (D = 32: +0.8 % C3 scan, its split-layout exact distances read the tail rows)
@@ -1912,10 +1912,12 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         STAMP(14)  // diagnostic split of "prep": loop top (into a2box's slot) vs the update chain
 #endif
         if (wave == 0 && has_p) vp_begin<C>(sh, P_buf, P_off, P_n, vq_a10, ln, lg_pos, lg_tag, vst);
-        // D = 8: the update chain right after its prep, so the V check can start
+        // The update chain right after its prep, so the V check can start
         // as soon as a wave is done with A1 (wave 0 reaches the mid-A1 barrier
         // early).  C5 -cs4 scan -3.2 % (5551 vs 5732 ms at 128 s) and no VGPR
-        // spill left; at D = 16 +0.6 % (3361 vs 3342 ms), so it stays after A1
+        // spill left; at D = 16 +0.6 % in round 4 (3361 vs 3342 ms), -1.5 % with
+        // round 6's in-batch DFS answers (3221 / 3225 vs 3269 / 3277 ms); D = 32
+        // (C3) -2.9 % (2750 / 2768 vs 2836 / 2841 ms)
         constexpr bool kVpEarly = D <= GSC_VP_EARLY_D;
         if constexpr (kVpEarly) {
             if (wave == 0 && has_p) {
