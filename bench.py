@@ -68,8 +68,8 @@ CORPUS = ROOT / "tests" / "golden" / "lame_test"
 
 VALU_F32_PEAK_TOPS = 78.6  # non-fused f32 VALU ops/s: half the 157.3 TFLOPS FMA-counted peak
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md (spec)
-PMC_SUMMARY = ROOT / "profiles" / "r05" / "pmc_summary.json"  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
-SQ_SUMMARY = ROOT / "profiles" / "r05" / "pmc_sq_summary.json"  # rocprofv3 --pmc SQ_* pass (tools/sq_summary.py)
+PMC_SUMMARY = ROOT / "profiles" / "r06" / "pmc_summary.json"  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
+SQ_SUMMARY = ROOT / "profiles" / "r06" / "pmc_sq_summary.json"  # rocprofv3 --pmc SQ_* pass (tools/sq_summary.py)
 DIGESTS = ROOT / "tests" / "golden" / "bench_digests.json"  # oracle per-frame .gsc digests (make_bench_digests.py)
 # oracle .gsc digests of the lame_test files (tests/golden/make_corpus.py)
 CORPUS_META = {"c4": ROOT / "tests" / "golden" / "corpus_meta.json",
