@@ -117,3 +117,65 @@ def test_bench_frame_digest_check(tmp_path, monkeypatch):
     assert bench.frame_digest_check("c2:8", 2, blob, sizes, 6)[1] == 1  # another frame cut
     assert bench.frame_digest_check("c2:9", 0, blob, sizes, 5) == (0, 0, 0)  # no digests: unchecked
     assert bench.frame_digest_check("c2:8", 2, blob + b"!", sizes, 5)[1] == 1  # bytes past the frames
+
+
+@pytest.mark.parametrize("args", [["--share", "1/8"], ["--share", "8/8", "--strong"],
+                                  ["--share", "1/8", "--strong", "--gpus", "2"]])
+def test_bench_refuses_bad_share(args):
+    """--share R/N (one rank's share of the whole file on one GPU) needs
+    --strong, --gpus 1 and 0 <= R < N; it is refused before any GPU call."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--no-cpu-baseline", *args], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "--share" in r.stderr
+
+
+def test_share_ranges_tile_the_whole_file():
+    """Every rank's --share range of the whole file's frame cut, for N = 1, 2,
+    4, 8: contiguous, in rank order, covering every frame once (the ranges an
+    N-GPU strong run gives its ranks, bench.py's bounds_range)."""
+    import oracle_ffi
+    from soundchunks_amd.shard import bounds_range
+    from soundchunks_amd.synth import synth_wav
+
+    wav = synth_wav(120.0, 48000, 2)
+    st, en = oracle_ffi.frame_bounds(wav, ["-cs4", "-cpf4096"])
+    for n in (1, 2, 4, 8):
+        rs = [bounds_range(st, en, 4, 2, r, n) for r in range(n)]
+        assert rs[0][0] == 0 and rs[-1][1] == len(st)
+        assert all(rs[r][1] == rs[r + 1][0] for r in range(n - 1))
+        assert all(b < e for b, e in rs)  # 30 frames: every rank gets some
+
+
+def _one_rank_worker(port, q):
+    sys.path[:0] = [str(ROOT), str(ROOT / "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from soundchunks_amd.shard import broadcast_bounds, gather_files, gather_streams
+
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        st, en = broadcast_bounds(np.array([0, 10, 20]), np.array([9, 19, 29]))
+        q.put((st.tolist(), en.tolist(), gather_streams(b"abc"), gather_streams(b""),
+               gather_files(b"aabbb", [2, 3])))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_one_rank_group_gathers():
+    """bench.py at --gpus 1 under a launcher (or --dist) runs the same
+    collectives in a one-rank group (RCCL on the GPU box, tests/test_gpu_rccl.py;
+    gloo here): the broadcast and both gathers are the identity."""
+    from soundchunks_amd.shard import free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_one_rank_worker, args=(free_port(), q))
+    p.start()
+    st, en, whole, empty, files = q.get(timeout=100)
+    p.join(30)
+    assert p.exitcode == 0
+    assert (st, en) == ([0, 10, 20], [9, 19, 29])
+    assert whole == b"abc" and empty == b"" and files == [b"aa", b"bbb"]
