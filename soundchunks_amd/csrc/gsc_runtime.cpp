@@ -415,8 +415,9 @@ int run_reduce_batch_dev(int D, int K, int precision, const std::vector<int>& Ns
             for (int k = 0; k < 16; ++k) m[k] += double(fr[i].ystamps[k]) / double(nf) / double(K);
         std::fprintf(stderr,
                      "yakmo stamps [clk/pick]: chain pick %.0f fast %.0f slow %.0f wait %.0f (fast calls %.1f"
-                     " slow blocks %.1f) | dist pick+sdlo %.0f compute %.0f wait %.0f\n",
-                     m[0], m[1], m[2], m[3], m[4], m[5], m[8], m[9], m[10]);
+                     " slow blocks %.1f) | dist pick+sdlo %.0f compute %.0f wait %.0f | negative deltas dropped"
+                     " per pick: chain %.3g dist %.3g\n",
+                     m[0], m[1], m[2], m[3], m[4], m[5], m[8], m[9], m[10], m[6], m[14]);
     }
     iters->resize(size_t(nf));
     slow->resize(size_t(nf));

@@ -64,12 +64,19 @@ __device__ __forceinline__ uint64_t ystamp() {
     __builtin_amdgcn_sched_barrier(0);
     return t;
 }
+// a delta that comes out negative (s_memtime read backwards once: round 5's
+// "slow" slot carried one frame's wrapped sum, 2^64 / (frames x picks)) is
+// not added but counted in slot 6 (wave 0) / 14 (distance waves)
 #define YST_DECL uint64_t yacc[16] = {}; uint64_t ylast = ystamp();
-#define YST(k)                     \
-    {                              \
-        const uint64_t t_ = ystamp(); \
-        yacc[k] += t_ - ylast;     \
-        ylast = t_;                \
+#define YST(k)                                      \
+    {                                               \
+        const uint64_t t_ = ystamp();               \
+        const int64_t d_ = (int64_t)(t_ - ylast);   \
+        if (d_ >= 0)                                \
+            yacc[k] += (uint64_t)d_;                \
+        else                                        \
+            yacc[(k) < 8 ? 6 : 14] += 1;            \
+        ylast = t_;                                 \
     }
 #define YCNT(k) yacc[k] += 1;
 #else
