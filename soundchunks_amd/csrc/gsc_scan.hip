@@ -162,7 +162,10 @@ __device__ __forceinline__ uint32_t rec_sib(const WaveRecT<SL>& r, int ls, int i
 
 // improvements of ANN's DFS kept per query for the in-batch DFS answers (valid
 // == 2 below): a DFS with more keeps its query uncertified (solo resolution)
-constexpr int kMaxImp = 8;
+#ifndef GSC_MAX_IMP
+#define GSC_MAX_IMP 8
+#endif
+constexpr int kMaxImp = GSC_MAX_IMP;
 
 template <int D>
 struct QRecT {        // A2 output per query
@@ -2237,6 +2240,14 @@ __global__ __launch_bounds__(C::NT) void scan_batch_kernel(ReduceFrame* __restri
         // every wave folds the committed updates of the centroids it owns, straight
         // from the update chain's rows (no barrier after the commit decision)
         if (kc > 0) fold_commits<C>(sh, creg, cn, cnmax, vwave, ln, P_buf, P_off, kc, it & 1, trow);
+#ifdef GSC_BOX_SHRINK
+        // experiment: the pruning boxes only grow within a pass (every fold widens
+        // them); re-fit them to the registers every GSC_BOX_SHRINK iterations (the
+        // next A1's snapshot is these registers; the solo below grows them again)
+        if constexpr (!C::SPLIT) {
+            if ((it % GSC_BOX_SHRINK) == GSC_BOX_SHRINK - 1) wave_box_init<C>(sh, creg, vwave, ln, p0, dmask);
+        }
+#endif
         STAMP(3)
         // ---- part 3: bookkeeping of the committed prefix
         ln = opaque_v(ln);
