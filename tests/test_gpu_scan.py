@@ -139,3 +139,29 @@ def test_scan_nan_centroids_k4096(oracle):
     nan = np.isnan(oc)
     np.testing.assert_array_equal(np.isnan(gc), nan)
     np.testing.assert_array_equal(_bits(np.where(nan, 0, gc)), _bits(np.where(nan, 0, oc)))
+
+
+@pytest.mark.parametrize("d,k", [(8, 1024), (8, 4096), (16, 4096)])
+def test_scan_integer_grid_ties_match_oracle(oracle, d, k):
+    """Integer-valued features with duplicate points: exact distance ties
+    everywhere, so many batch queries get no certificate (no unique minimum)
+    and take ANN's own DFS answer on the snapshot (gsc_scan.hip's in-batch
+    DFS answers, checked at the commit by dfs_keeps), and moved centroids
+    land on exact ties with them.  Three passes, bit-exact against the oracle's
+    KNNScanReduce (encoder.lpr:699-765 over ANN's stale tree)."""
+    import soundchunks_amd as sc
+
+    rng = np.random.default_rng(7 + d + k)
+    n = 24000
+    x = rng.integers(-6, 7, size=(n, d)).astype(np.float32)
+    x[::5] = x[1::5][: len(x[::5])]  # runs of duplicate points
+    c0 = x[rng.choice(n, k, replace=False)] + rng.integers(-1, 2, size=(k, d)).astype(np.float32) * 0.5
+    os.environ["GSC_SCAN_MAX_PASSES"] = "3"
+    try:
+        gc, gcl, gn = sc.scan_reduce(x, c0, precision=3)
+    finally:
+        del os.environ["GSC_SCAN_MAX_PASSES"]
+    oc, ocl, on = oracle.scan_reduce(x, c0, 3, 3)
+    assert gn == on
+    np.testing.assert_array_equal(gcl, ocl)
+    np.testing.assert_array_equal(_bits(gc), _bits(oc))
